@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""bench.py — Inception-v3 299x299 training throughput on MI355X (libjr).
+
+Metric (BASELINE.json): train images/sec, Inception-v3 299^2 bs64/GPU,
+1-8 MI355X; % MFMA peak.  One step = forward + backward + gradient
+all-reduce (N>1) + Nesterov update of one 64-image batch per GPU, the
+reference's train.py:231-232 sess.run.  N=1 workload: BASELINE configs[1]
+(fp32, batch 64, one GPU).  Synthetic fundus-shaped inputs (jr.synth),
+resident in HBM before timing; Keras-default random init (App. C Q2).
+
+  python bench.py [--gpus N --steps K --warmup W --dtype f32]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  `roofline` is for the conv implicit-GEMM
+family (the dominant kernels): algorithmic conv FLOPs per step / summed conv
+op time per step, both from an instrumented pass (HIP events around every
+conv call on the engine stream) run right after the timed region.
+`cpu_baseline` times oracle/inception_ref.py (torch-CPU fp32 restatement,
+kind "port") on the host cores for a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "jama16-retina-replication_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--res", type=int, default=299)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a HIP graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=64)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def conv_roofline(eng, steps: int = 3):
+    """Instrumented eager pass: HIP events (torch.cuda.Event on eng.stream)
+    bracket every conv fwd/dgrad/wgrad call; returns (flops/step, conv s/step)."""
+    from jr import _ffi
+    fwd, bwd, opt, _ = eng._build_calls(eng.batch)
+    conv_names = {"conv_fwd", "conv_dgrad", "conv_wgrad"}
+    flops = 0
+    for n in eng.g.convs:
+        m = n.macs_per_image() * eng.batch
+        flops += 2 * m * (2 if n.x == eng.g.input_buf else 3)
+    pairs = []
+    for _ in range(steps):
+        for calls in (fwd, bwd, opt):
+            for fn, args, name in calls:
+                if fn == "param_ready":
+                    continue
+                if name in conv_names:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(eng.stream)
+                    rc = fn(*args)
+                    e1.record(eng.stream)
+                    pairs.append((e0, e1))
+                else:
+                    rc = fn(*args)
+                if rc:
+                    raise _ffi.JRError(name, rc, _ffi.last_error())
+    eng.synchronize()
+    t = sum(a.elapsed_time(b) for a, b in pairs) / 1e3 / steps
+    return flops, t, len(pairs) // steps
+
+
+def cpu_baseline(args, res):
+    from jr.inception import build_inception_v3
+    from jr.init import init_params, unflatten
+    from jr import synth
+    from oracle.inception_ref import InceptionV3Ref
+    cores = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    g = build_inception_v3(res, res)
+    ref = InceptionV3Ref(unflatten(g, init_params(g, 0)), torch.float32)
+    B = args.cpu_batch
+    x = synth.fundus_batch(0, B, res).astype(np.float32) * np.float32(1 / 255)
+    y = synth.labels(0, B)
+    st = {}
+    ref.train_step(x, y, st)   # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        ref.train_step(x, y, st)
+    dt = time.perf_counter() - t0
+    return {"value": round(B * args.cpu_steps / dt, 3), "unit": "images/sec", "cores": cores, "kind": "port",
+            "sample": f"{args.cpu_steps} timed train steps (+1 warm-up) of batch {B} at {res}x{res} fp32, "
+                      f"torch-CPU restatement oracle/inception_ref.py ({dt:.1f} s)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if rank == 0 and world > 1:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from jr.engine import Engine
+    from jr import synth
+    from jr.dist import BucketAllReduce
+
+    B, res = args.batch, args.res
+    eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0)
+    imgs = synth.fundus_batch(rank * B, B, res)
+    labels = synth.labels(rank * B, B)
+    eng.set_batch(imgs, labels)
+    eng.synchronize()
+    ar = BucketAllReduce(eng, world) if world > 1 else None
+    use_graph = (not args.no_graph) and ar is None
+
+    def step():
+        if use_graph:
+            eng.replay()
+        else:
+            eng.train_step(allreduce=ar)
+
+    for i in range(args.warmup):
+        if use_graph and i == 0:
+            eng.train_step()           # first step eager (plans, workspaces)
+            eng.synchronize()
+            eng.capture()
+            continue
+        step()
+    if use_graph and args.warmup == 0:
+        eng.capture()
+    eng.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = eng.loss_value()
+    if not np.isfinite(loss):
+        raise SystemExit(f"non-finite loss {loss}")
+
+    out = None
+    if rank == 0:
+        imgs_s = B * world * args.steps / elapsed
+        ms = elapsed / args.steps * 1e3
+        roof = None
+        if not args.no_roofline:
+            flops, tconv, nconv = conv_roofline(eng)
+            ach = flops / tconv / 1e12
+            peak = PEAK_TFLOPS[args.dtype]
+            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(ach / peak, 4), "traffic": None,
+                    "kernel": f"conv implicit-GEMM fwd+dgrad+wgrad ({nconv} calls/step)",
+                    "conv_ms_per_step": round(tconv * 1e3, 3),
+                    "algorithmic_gflop_per_step": round(flops / 1e9, 1)}
+        out = {
+            "metric": "train images/sec, Inception-v3 299^2 bs64/GPU",
+            "value": round(imgs_s, 2), "unit": "images/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.dtype, "data": "synthetic fundus-shaped uint8 299x299x3 (jr.synth), random Keras init",
+            "config": {"workload": f"Inception-v3 {res}x{res} {args.dtype} training, batch {B}/GPU, "
+                                   f"Nesterov lr 3e-3 m 0.9", "model": "inception_v3", "global_batch": B * world,
+                       "seq_len": None, "parallelism": f"dp{world}", "hip_graph": use_graph},
+            "final_loss": round(loss, 5),
+            "roofline": roof,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args, res)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

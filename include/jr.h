@@ -1,0 +1,169 @@
+/*
+ * jr.h — C-ABI of libjr.so, the MI355X (gfx950) compute library behind the
+ * jama16-retina-replication hot path: the Inception-v3 training step and
+ * ensemble inference of train.py / evaluate.py.
+ *
+ * The reference has no FFI: every op below replaces a TensorFlow op that the
+ * reference graph instantiates.  Each entry point cites the
+ * reference call site whose TF op it replaces.
+ *
+ * Conventions
+ *  - Every function returns JR_OK (0) or a negative jr_status; the message of
+ *    the last failure on the calling thread is returned by jr_last_error().
+ *  - All tensor arguments are caller-owned DEVICE pointers (torch.Tensor
+ *    .data_ptr() on the host side).  The library never allocates, except that
+ *    multi-kernel ops take a caller-provided workspace sized by the matching
+ *    *_workspace_size query.
+ *  - Activations are NHWC (channels_last, lib/dataset.py:42-43); conv kernels
+ *    are HWIO [kh][kw][cin][cout] (the Keras Conv2D layout).
+ *  - A channel slice (c_off, c_stride) addresses channels
+ *    [c_off, c_off + c) of a buffer whose pixel rows hold c_stride channels;
+ *    this is how Inception-block outputs are written concat-free.
+ *  - No host synchronisation inside any call; every call is enqueued on the
+ *    given stream (hipStream_t passed as void*; NULL = the null stream), so a
+ *    whole training step can be captured into a HIP graph.
+ *  - dtype: JR_F32 = IEEE fp32 end to end (the reference's precision);
+ *    JR_BF16 = bf16 activations/weights with fp32 accumulation.
+ */
+#ifndef JR_H_
+#define JR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum jr_status {
+  JR_OK = 0,
+  JR_ERR_INVALID = -1,     /* bad argument / unsupported geometry          */
+  JR_ERR_HIP = -2,         /* a HIP runtime call failed                    */
+  JR_ERR_UNSUPPORTED = -3, /* valid request this build does not implement  */
+  JR_ERR_WORKSPACE = -4    /* workspace smaller than *_workspace_size      */
+} jr_status;
+
+typedef enum jr_dtype { JR_F32 = 0, JR_BF16 = 1 } jr_dtype;
+
+typedef enum jr_conv_op { JR_CONV_FWD = 0, JR_CONV_BWD_DATA = 1, JR_CONV_BWD_FILTER = 2 } jr_conv_op;
+
+typedef enum jr_head_mode { JR_HEAD_SIGMOID = 0, JR_HEAD_SOFTMAX = 1 } jr_head_mode;
+
+/* One Conv2D(use_bias=False) layer of keras_applications inception_v3
+ * conv2d_bn (instantiated at train.py:129-130).  pad_* are the top/left
+ * paddings: 'same' at stride 1 => (k-1)/2, 'valid' => 0. */
+typedef struct jr_conv_desc {
+  int32_t n, h, w, c_in;          /* input  [n, h, w, c_in] (slice)        */
+  int32_t c_out, kh, kw;          /* kernel [kh, kw, c_in, c_out]          */
+  int32_t stride_h, stride_w;
+  int32_t pad_h, pad_w;
+  int32_t ho, wo;                 /* output [n, ho, wo, c_out] (slice)     */
+  int32_t x_c_off, x_c_stride;    /* channel slice of the input buffer     */
+  int32_t y_c_off, y_c_stride;    /* channel slice of the output buffer    */
+} jr_conv_desc;
+
+/* 3x3 pooling window; max: stride 2 'valid', avg: stride 1 'same' with the
+ * TF exclude-padding divisor. */
+typedef struct jr_pool_desc {
+  int32_t n, h, w, c;
+  int32_t ho, wo;
+  int32_t x_c_off, x_c_stride;
+  int32_t y_c_off, y_c_stride;
+} jr_pool_desc;
+
+/* ---- library ---------------------------------------------------------- */
+int jr_init(int device);
+const char* jr_last_error(void);
+const char* jr_version(void);
+
+/* ---- convolution (train.py:129-130 -> Keras Conv2D -> TF Conv2D,
+ *      Conv2DBackpropInput, Conv2DBackpropFilter created by .minimize at
+ *      train.py:150-153) ----------------------------------------------- */
+size_t jr_conv2d_workspace_size(const jr_conv_desc* d, int op, int dtype);
+/* y[.., y_c_off + co] = sum x * w   (raw conv output, no bias) */
+int jr_conv2d_fwd(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y,
+                  void* ws, size_t ws_bytes, void* stream);
+/* dx[.., x_c_off + ci] (+)= sum dy * w ; accumulate != 0 adds into dx */
+int jr_conv2d_bwd_data(const jr_conv_desc* d, int dtype, const void* dy, const void* w, void* dx,
+                       int accumulate, void* ws, size_t ws_bytes, void* stream);
+/* dw[kh][kw][ci][co] = sum x * dy  (fp32 output for both dtypes) */
+int jr_conv2d_bwd_filter(const jr_conv_desc* d, int dtype, const void* x, const void* dy, float* dw,
+                         void* ws, size_t ws_bytes, void* stream);
+
+/* ---- BatchNormalization(scale=False, eps) + ReLU, training-mode batch
+ *      statistics (Keras conv2d_bn; App. C Q1: always batch stats) ----- */
+size_t jr_bn_workspace_size(int64_t m, int32_t c);
+/* x: raw conv output [m][c] contiguous.  mean/invstd: [c] fp32 outputs.
+ * invstd = 1/sqrt(biased_var + eps). */
+int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps, float* mean, float* invstd,
+                void* ws, size_t ws_bytes, void* stream);
+/* y[.., y_c_off + k] = max((x - mean) * invstd + beta, 0) */
+int jr_bn_relu_apply(int dtype, const void* x, int64_t m, int32_t c, const float* mean,
+                     const float* invstd, const float* beta, void* y, int32_t y_c_off,
+                     int32_t y_c_stride, void* stream);
+/* Backward of apply+stats: dy is the gradient w.r.t. y (a channel slice),
+ * dx [m][c] contiguous receives the gradient w.r.t. the raw conv output,
+ * dbeta [c] receives sum of the ReLU-masked dy. */
+int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t dy_c_stride, const void* x,
+                   int64_t m, int32_t c, const float* mean, const float* invstd, const float* beta,
+                   void* dx, float* dbeta, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- pooling (Keras MaxPooling2D((3,3),(2,2)) / AveragePooling2D((3,3),
+ *      (1,1),'same') inside InceptionV3, train.py:129-130) ------------ */
+/* argmax [n][ho][wo][c] uint8 (window position 0..8, first max in scan
+ * order) is written by fwd when non-NULL and routes the gradient in bwd. */
+int jr_maxpool3x3s2_fwd(const jr_pool_desc* d, int dtype, const void* x, void* y, uint8_t* argmax,
+                        void* stream);
+int jr_maxpool3x3s2_bwd(const jr_pool_desc* d, int dtype, const uint8_t* argmax, const void* dy,
+                        void* dx, int accumulate, void* stream);
+int jr_avgpool3x3s1_fwd(const jr_pool_desc* d, int dtype, const void* x, void* y, void* stream);
+int jr_avgpool3x3s1_bwd(const jr_pool_desc* d, int dtype, const void* dy, void* dx, int accumulate,
+                        void* stream);
+
+/* ---- GlobalAveragePooling2D (pooling='avg', train.py:130) ------------ */
+int jr_gap_fwd(int dtype, const void* x, int32_t n, int32_t hw, int32_t c, float* y, void* stream);
+int jr_gap_bwd(int dtype, const float* dy, int32_t n, int32_t hw, int32_t c, void* dx, void* stream);
+
+/* ---- head: tf.layers.dense(units) (train.py:133) + tf.sigmoid
+ *      'predictions' (train.py:136) + reduce_mean(sigmoid xent)
+ *      (train.py:140-141).  Softmax mode = softmax cross-entropy.
+ *      labels may be NULL (inference: loss not computed). ----------- */
+int jr_head_fwd(int mode, const float* feat, const float* w, const float* b, const float* labels,
+                int32_t n, int32_t c, int32_t units, float* logits, float* probs, float* loss,
+                void* stream);
+int jr_head_bwd(int mode, const float* feat, const float* w, const float* probs, const float* labels,
+                int32_t n, int32_t c, int32_t units, float* dfeat, float* dw, float* db, void* stream);
+
+/* ---- optimizers (train.py:147-153: GradientDescentOptimizer /
+ *      MomentumOptimizer(use_nesterov=True) -> TF ApplyMomentum) ------- */
+/* accum = accum*momentum + g; w -= g*lr + accum*momentum*lr   (g = grad*grad_scale) */
+int jr_nesterov_update(float* w, const float* grad, float* accum, int64_t n, float lr,
+                       float momentum, float grad_scale, void* stream);
+/* plain momentum (use_nesterov=False): accum = accum*m + g; w -= lr*accum */
+int jr_momentum_update(float* w, const float* grad, float* accum, int64_t n, float lr,
+                       float momentum, float grad_scale, void* stream);
+int jr_sgd_update(float* w, const float* grad, int64_t n, float lr, float grad_scale, void* stream);
+/* Adam (north-star extra, not in the reference): TF AdamOptimizer form */
+int jr_adam_update(float* w, const float* grad, float* m, float* v, int64_t n, float lr_t,
+                   float beta1, float beta2, float eps, float grad_scale, void* stream);
+
+/* ---- dtype helpers --------------------------------------------------- */
+int jr_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream);
+int jr_cast_bf16_to_f32(const void* src, float* dst, int64_t n, void* stream);
+/* uint8 HWC images -> f32 * f32(1/255) (tf.image.convert_image_dtype,
+ * lib/dataset.py:20-21) */
+int jr_u8_to_f32_scaled(const uint8_t* src, void* dst, int dtype, int64_t n, void* stream);
+/* acc[0] += sum (p - y)^2, acc[1] += n   (tf.metrics.mean_squared_error,
+ * train.py:175-177) */
+int jr_brier_accumulate(const float* probs, const float* labels, int32_t n, double* acc, void* stream);
+
+/* ---- HIP graph capture of a whole step ------------------------------ */
+int jr_graph_begin(void* stream);
+int jr_graph_end(void* stream, void** graph_exec);
+int jr_graph_launch(void* graph_exec, void* stream);
+int jr_graph_destroy(void* graph_exec);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JR_H_ */

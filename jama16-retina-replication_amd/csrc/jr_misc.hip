@@ -1,0 +1,192 @@
+// jr_misc.hip — optimizers, dtype casts, input scaling, Brier accumulator.
+//
+// Optimizers replace the TF ApplyMomentum / ApplyGradientDescent ops that
+// .minimize adds at train.py:147-153.  One launch updates
+// the whole flat parameter buffer (21,770,401 fp32 values); each lane moves
+// 16-byte vectors and the arithmetic is written with explicit _rn intrinsics
+// so it is the unfused TF expression order:
+//   ApplyMomentum(use_nesterov): accum = accum*m + g; var -= g*lr + accum*m*lr
+//   ApplyMomentum:               accum = accum*m + g; var -= accum*lr
+//   ApplyGradientDescent:        var -= g*lr
+#include "jr_common.h"
+
+namespace jr {
+
+static int grid_for(int64_t items) {
+  const int64_t b = ceil_div(items, 256);
+  return (int)std::min<int64_t>(std::max<int64_t>(b, 1), 256 * 32);
+}
+
+__device__ __forceinline__ float nest1(float& w, float g, float& a, float lr, float m) {
+  a = __fadd_rn(__fmul_rn(a, m), g);
+  w = __fsub_rn(w, __fadd_rn(__fmul_rn(g, lr), __fmul_rn(__fmul_rn(a, m), lr)));
+  return w;
+}
+
+__global__ void __launch_bounds__(256) k_nesterov(float* __restrict__ w, const float* __restrict__ grad,
+                                                  float* __restrict__ accum, int64_t n, float lr, float m,
+                                                  float gs) {
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 wv = reinterpret_cast<float4*>(w)[i];
+    float4 av = reinterpret_cast<float4*>(accum)[i];
+    const float4 gv = reinterpret_cast<const float4*>(grad)[i];
+    nest1(wv.x, __fmul_rn(gv.x, gs), av.x, lr, m);
+    nest1(wv.y, __fmul_rn(gv.y, gs), av.y, lr, m);
+    nest1(wv.z, __fmul_rn(gv.z, gs), av.z, lr, m);
+    nest1(wv.w, __fmul_rn(gv.w, gs), av.w, lr, m);
+    reinterpret_cast<float4*>(w)[i] = wv;
+    reinterpret_cast<float4*>(accum)[i] = av;
+  }
+  // tail
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < (n & 3)) {
+    const int64_t i = n4 * 4 + t;
+    nest1(w[i], __fmul_rn(grad[i], gs), accum[i], lr, m);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_momentum(float* __restrict__ w, const float* __restrict__ grad,
+                                                  float* __restrict__ accum, int64_t n, float lr, float m,
+                                                  float gs) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float g = __fmul_rn(grad[i], gs);
+    const float a = __fadd_rn(__fmul_rn(accum[i], m), g);
+    accum[i] = a;
+    w[i] = __fsub_rn(w[i], __fmul_rn(a, lr));
+  }
+}
+
+__global__ void __launch_bounds__(256) k_sgd(float* __restrict__ w, const float* __restrict__ grad, int64_t n,
+                                             float lr, float gs) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    w[i] = __fsub_rn(w[i], __fmul_rn(__fmul_rn(grad[i], gs), lr));
+}
+
+// TF ApplyAdam: m = m + (g - m)(1-b1); v = v + (g^2 - v)(1-b2);
+// var -= lr_t * m / (sqrt(v) + eps)   with lr_t = lr*sqrt(1-b2^t)/(1-b1^t) from the host.
+__global__ void __launch_bounds__(256) k_adam(float* __restrict__ w, const float* __restrict__ grad,
+                                              float* __restrict__ mm, float* __restrict__ vv, int64_t n,
+                                              float lr_t, float b1, float b2, float eps, float gs) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float g = grad[i] * gs;
+    const float m1 = mm[i] + (g - mm[i]) * (1.f - b1);
+    const float v1 = vv[i] + (g * g - vv[i]) * (1.f - b2);
+    mm[i] = m1;
+    vv[i] = v1;
+    w[i] -= lr_t * m1 / (sqrtf(v1) + eps);
+  }
+}
+
+__global__ void k_f32_to_bf16(const float* __restrict__ s, uint16_t* d, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    d[i] = f2bf(s[i]);
+}
+
+__global__ void k_bf16_to_f32(const uint16_t* __restrict__ s, float* d, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    d[i] = bf2f(s[i]);
+}
+
+// tf.image.convert_image_dtype(uint8 -> float32): f32(x) * f32(1/255)
+template <typename T>
+__global__ void k_u8_scale(const uint8_t* __restrict__ s, T* d, int64_t n) {
+  const float scale = 1.0f / 255.0f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    Elt<T>::st(d + i, __fmul_rn((float)s[i], scale));
+}
+
+__global__ void k_brier(const float* __restrict__ p, const float* __restrict__ y, int n, double* acc) {
+  __shared__ double red[256];
+  const int t = threadIdx.x;
+  double s = 0.0;
+  for (int i = t; i < n; i += 256) {
+    const double d = (double)p[i] - (double)y[i];
+    s += d * d;
+  }
+  red[t] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  if (t == 0) {
+    acc[0] += red[0];
+    acc[1] += (double)n;
+  }
+}
+
+}  // namespace jr
+
+using namespace jr;
+
+JR_API int jr_nesterov_update(float* w, const float* grad, float* accum, int64_t n, float lr, float momentum,
+                              float grad_scale, void* stream) {
+  if (!w || !grad || !accum || n < 0) return fail(JR_ERR_INVALID, "nesterov: bad arguments");
+  if (((uintptr_t)w | (uintptr_t)grad | (uintptr_t)accum) & 15)
+    return fail(JR_ERR_INVALID, "nesterov: buffers must be 16-byte aligned");
+  if (n == 0) return JR_OK;
+  hipLaunchKernelGGL(k_nesterov, dim3(grid_for(std::max<int64_t>(n / 4, 4))), dim3(256), 0, as_stream(stream), w,
+                     grad, accum, n, lr, momentum, grad_scale);
+  return check_launch("nesterov");
+}
+
+JR_API int jr_momentum_update(float* w, const float* grad, float* accum, int64_t n, float lr, float momentum,
+                              float grad_scale, void* stream) {
+  if (!w || !grad || !accum || n < 0) return fail(JR_ERR_INVALID, "momentum: bad arguments");
+  if (n == 0) return JR_OK;
+  hipLaunchKernelGGL(k_momentum, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), w, grad, accum, n, lr,
+                     momentum, grad_scale);
+  return check_launch("momentum");
+}
+
+JR_API int jr_sgd_update(float* w, const float* grad, int64_t n, float lr, float grad_scale, void* stream) {
+  if (!w || !grad || n < 0) return fail(JR_ERR_INVALID, "sgd: bad arguments");
+  if (n == 0) return JR_OK;
+  hipLaunchKernelGGL(k_sgd, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), w, grad, n, lr, grad_scale);
+  return check_launch("sgd");
+}
+
+JR_API int jr_adam_update(float* w, const float* grad, float* m, float* v, int64_t n, float lr_t, float beta1,
+                          float beta2, float eps, float grad_scale, void* stream) {
+  if (!w || !grad || !m || !v || n < 0) return fail(JR_ERR_INVALID, "adam: bad arguments");
+  if (n == 0) return JR_OK;
+  hipLaunchKernelGGL(k_adam, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), w, grad, m, v, n, lr_t, beta1,
+                     beta2, eps, grad_scale);
+  return check_launch("adam");
+}
+
+JR_API int jr_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream) {
+  if (!src || !dst || n < 0) return fail(JR_ERR_INVALID, "cast: bad arguments");
+  if (n == 0) return JR_OK;
+  hipLaunchKernelGGL(k_f32_to_bf16, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), src, (uint16_t*)dst, n);
+  return check_launch("cast f32->bf16");
+}
+
+JR_API int jr_cast_bf16_to_f32(const void* src, float* dst, int64_t n, void* stream) {
+  if (!src || !dst || n < 0) return fail(JR_ERR_INVALID, "cast: bad arguments");
+  if (n == 0) return JR_OK;
+  hipLaunchKernelGGL(k_bf16_to_f32, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), (const uint16_t*)src, dst,
+                     n);
+  return check_launch("cast bf16->f32");
+}
+
+JR_API int jr_u8_to_f32_scaled(const uint8_t* src, void* dst, int dtype, int64_t n, void* stream) {
+  if (!src || !dst || n < 0) return fail(JR_ERR_INVALID, "u8_scale: bad arguments");
+  if (n == 0) return JR_OK;
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_u8_scale<float>, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), src, (float*)dst, n);
+  else if (dtype == JR_BF16)
+    hipLaunchKernelGGL(k_u8_scale<uint16_t>, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), src,
+                       (uint16_t*)dst, n);
+  else
+    return fail(JR_ERR_INVALID, "u8_scale: bad dtype");
+  return check_launch("u8_scale");
+}
+
+JR_API int jr_brier_accumulate(const float* probs, const float* labels, int32_t n, double* acc, void* stream) {
+  if (!probs || !labels || !acc || n < 0) return fail(JR_ERR_INVALID, "brier: bad arguments");
+  if (n == 0) return JR_OK;
+  hipLaunchKernelGGL(k_brier, dim3(1), dim3(256), 0, as_stream(stream), probs, labels, n, acc);
+  return check_launch("brier");
+}

@@ -1,0 +1,310 @@
+// jr_pool.hip — Inception-v3 pooling ops, forward and backward, NHWC with
+// channel slices so pool outputs land directly in their concat buffer.
+//
+//  - MaxPooling2D((3,3), strides=(2,2)) 'valid' (stem x2, mixed3, mixed8 of
+//    the Keras InceptionV3 built at train.py:129-130).
+//    fwd writes the window argmax (first max in scan order, uint8) so bwd is
+//    a deterministic gather: every input element sums the dy of the (at most
+//    2x2) windows whose argmax it is.
+//  - AveragePooling2D((3,3), strides=(1,1), padding='same') (mixed0-2, 4-7,
+//    9-10; a7): TF divides by the number of in-bounds taps (exclude padding).
+//  - GlobalAveragePooling2D (pooling='avg', train.py:130; a9).
+// All kernels move fp32x4 (or bf16x4) vectors along the channel axis.
+#include "jr_common.h"
+
+namespace jr {
+
+template <typename T> struct P4;
+template <> struct P4<float> {
+  __device__ static float4 ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  __device__ static void st(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+};
+template <> struct P4<uint16_t> {
+  __device__ static float4 ld(const uint16_t* p) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+  }
+  __device__ static void st(uint16_t* p, float4 v) {
+    uint2 u;
+    u.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+    u.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+    *reinterpret_cast<uint2*>(p) = u;
+  }
+};
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_maxpool_fwd(jr_pool_desc d, const T* __restrict__ x, T* y,
+                                                     uint8_t* argmax) {
+  const int c4 = d.c >> 2;
+  const int64_t total = (int64_t)d.n * d.ho * d.wo * c4;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(e % c4);
+    const int64_t pix = e / c4;
+    const int ow = (int)(pix % d.wo);
+    const int64_t t = pix / d.wo;
+    const int oh = (int)(t % d.ho);
+    const int b = (int)(t / d.ho);
+    float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int arg[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int ih = oh * 2 + r, iw = ow * 2 + c;
+        const float4 v = P4<T>::ld(x + ((int64_t)(b * d.h + ih) * d.w + iw) * d.x_c_stride + d.x_c_off + q * 4);
+        const float va[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (va[j] > best[j] || (r == 0 && c == 0)) { best[j] = va[j]; arg[j] = r * 3 + c; }
+      }
+    }
+    P4<T>::st(y + pix * d.y_c_stride + d.y_c_off + q * 4, make_float4(best[0], best[1], best[2], best[3]));
+    if (argmax) {
+      const uint32_t packed = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) |
+                              ((uint32_t)arg[3] << 24);
+      *reinterpret_cast<uint32_t*>(argmax + pix * d.c + q * 4) = packed;
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_maxpool_bwd(jr_pool_desc d, const uint8_t* __restrict__ argmax,
+                                                     const T* __restrict__ dy, T* dx, int accumulate) {
+  const int c4 = d.c >> 2;
+  const int64_t total = (int64_t)d.n * d.h * d.w * c4;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(e % c4);
+    const int64_t pix = e / c4;
+    const int iw = (int)(pix % d.w);
+    const int64_t t = pix / d.w;
+    const int ih = (int)(t % d.h);
+    const int b = (int)(t / d.h);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int oh_lo = max(0, (ih - 1) / 2), oh_hi = min(d.ho - 1, ih / 2);
+    const int ow_lo = max(0, (iw - 1) / 2), ow_hi = min(d.wo - 1, iw / 2);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int pos = (ih - oh * 2) * 3 + (iw - ow * 2);
+        const int64_t op = ((int64_t)b * d.ho + oh) * d.wo + ow;
+        const uint32_t am = *reinterpret_cast<const uint32_t*>(argmax + op * d.c + q * 4);
+        const float4 g = P4<T>::ld(dy + op * d.y_c_stride + d.y_c_off + q * 4);
+        const float ga[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if ((int)((am >> (8 * j)) & 0xff) == pos) acc[j] += ga[j];
+      }
+    }
+    T* p = dx + pix * d.x_c_stride + d.x_c_off + q * 4;
+    float4 o = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    if (accumulate) o = f4add(o, P4<T>::ld(p));
+    P4<T>::st(p, o);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_avgpool_fwd(jr_pool_desc d, const T* __restrict__ x, T* y) {
+  const int c4 = d.c >> 2;
+  const int64_t total = (int64_t)d.n * d.ho * d.wo * c4;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(e % c4);
+    const int64_t pix = e / c4;
+    const int ow = (int)(pix % d.wo);
+    const int64_t t = pix / d.wo;
+    const int oh = (int)(t % d.ho);
+    const int b = (int)(t / d.ho);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int cnt = 0;
+    for (int r = -1; r <= 1; ++r) {
+      const int ih = oh + r;
+      if ((unsigned)ih >= (unsigned)d.h) continue;
+      for (int c = -1; c <= 1; ++c) {
+        const int iw = ow + c;
+        if ((unsigned)iw >= (unsigned)d.w) continue;
+        s = f4add(s, P4<T>::ld(x + ((int64_t)(b * d.h + ih) * d.w + iw) * d.x_c_stride + d.x_c_off + q * 4));
+        ++cnt;
+      }
+    }
+    const float fc = (float)cnt;
+    P4<T>::st(y + pix * d.y_c_stride + d.y_c_off + q * 4, make_float4(s.x / fc, s.y / fc, s.z / fc, s.w / fc));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_avgpool_bwd(jr_pool_desc d, const T* __restrict__ dy, T* dx,
+                                                     int accumulate) {
+  const int c4 = d.c >> 2;
+  const int64_t total = (int64_t)d.n * d.h * d.w * c4;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(e % c4);
+    const int64_t pix = e / c4;
+    const int iw = (int)(pix % d.w);
+    const int64_t t = pix / d.w;
+    const int ih = (int)(t % d.h);
+    const int b = (int)(t / d.h);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = -1; r <= 1; ++r) {
+      const int oh = ih + r;
+      if ((unsigned)oh >= (unsigned)d.ho) continue;
+      const int ch = 1 + (oh > 0) + (oh < d.h - 1);
+      for (int c = -1; c <= 1; ++c) {
+        const int ow = iw + c;
+        if ((unsigned)ow >= (unsigned)d.wo) continue;
+        const int cw = 1 + (ow > 0) + (ow < d.w - 1);
+        const float fc = (float)(ch * cw);
+        const float4 g = P4<T>::ld(dy + (((int64_t)b * d.ho + oh) * d.wo + ow) * d.y_c_stride + d.y_c_off + q * 4);
+        s = f4add(s, make_float4(g.x / fc, g.y / fc, g.z / fc, g.w / fc));
+      }
+    }
+    T* p = dx + pix * d.x_c_stride + d.x_c_off + q * 4;
+    if (accumulate) s = f4add(s, P4<T>::ld(p));
+    P4<T>::st(p, s);
+  }
+}
+
+// GAP: one thread per (b, channel quad), loop over hw in order.
+template <typename T>
+__global__ void k_gap_fwd(const T* __restrict__ x, int n, int hw, int c, float* y) {
+  const int c4 = c >> 2;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * c4) return;
+  const int b = e / c4, q = e - b * c4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int p = 0; p < hw; ++p) s = f4add(s, P4<T>::ld(x + ((int64_t)b * hw + p) * c + q * 4));
+  const float f = (float)hw;
+  *reinterpret_cast<float4*>(y + (int64_t)b * c + q * 4) = make_float4(s.x / f, s.y / f, s.z / f, s.w / f);
+}
+
+template <typename T>
+__global__ void k_gap_bwd(const float* __restrict__ dy, int n, int hw, int c, T* dx) {
+  const int c4 = c >> 2;
+  const int64_t total = (int64_t)n * hw * c4;
+  const float f = (float)hw;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(e % c4);
+    const int64_t pix = e / c4;
+    const int b = (int)(pix / hw);
+    const float4 g = *reinterpret_cast<const float4*>(dy + (int64_t)b * c + q * 4);
+    P4<T>::st(dx + pix * c + q * 4, make_float4(g.x / f, g.y / f, g.z / f, g.w / f));
+  }
+}
+
+static int grid_for(int64_t items) {
+  const int64_t b = ceil_div(items, 256);
+  return (int)std::min<int64_t>(std::max<int64_t>(b, 1), 256 * 16);
+}
+
+static int check_pool(const jr_pool_desc* d, int dtype, bool maxpool) {
+  if (!d) return fail(JR_ERR_INVALID, "pool: null descriptor");
+  if (dtype != JR_F32 && dtype != JR_BF16) return fail(JR_ERR_INVALID, "pool: bad dtype");
+  if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c <= 0) return fail(JR_ERR_INVALID, "pool: empty tensor");
+  if (d->c % 4 || d->x_c_off % 4 || d->x_c_stride % 4 || d->y_c_off % 4 || d->y_c_stride % 4)
+    return fail(JR_ERR_INVALID, "pool: channels, offsets and strides must be multiples of 4");
+  if (d->x_c_off < 0 || d->x_c_off + d->c > d->x_c_stride || d->y_c_off < 0 || d->y_c_off + d->c > d->y_c_stride)
+    return fail(JR_ERR_INVALID, "pool: channel slice out of range");
+  if (maxpool) {
+    if (d->h < 3 || d->w < 3 || d->ho != (d->h - 3) / 2 + 1 || d->wo != (d->w - 3) / 2 + 1)
+      return fail(JR_ERR_INVALID, "maxpool: ho/wo must be (h-3)/2+1 (3x3 stride 2 valid)");
+  } else {
+    if (d->ho != d->h || d->wo != d->w) return fail(JR_ERR_INVALID, "avgpool: 'same' stride 1 needs ho=h, wo=w");
+  }
+  return JR_OK;
+}
+
+}  // namespace jr
+
+using namespace jr;
+
+JR_API int jr_maxpool3x3s2_fwd(const jr_pool_desc* d, int dtype, const void* x, void* y, uint8_t* argmax,
+                               void* stream) {
+  int rc = check_pool(d, dtype, true);
+  if (rc) return rc;
+  if (!x || !y) return fail(JR_ERR_INVALID, "maxpool_fwd: null pointer");
+  const int g = grid_for((int64_t)d->n * d->ho * d->wo * (d->c / 4));
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_maxpool_fwd<float>, dim3(g), dim3(256), 0, as_stream(stream), *d, (const float*)x,
+                       (float*)y, argmax);
+  else
+    hipLaunchKernelGGL(k_maxpool_fwd<uint16_t>, dim3(g), dim3(256), 0, as_stream(stream), *d,
+                       (const uint16_t*)x, (uint16_t*)y, argmax);
+  return check_launch("maxpool_fwd");
+}
+
+JR_API int jr_maxpool3x3s2_bwd(const jr_pool_desc* d, int dtype, const uint8_t* argmax, const void* dy,
+                               void* dx, int accumulate, void* stream) {
+  int rc = check_pool(d, dtype, true);
+  if (rc) return rc;
+  if (!argmax || !dy || !dx) return fail(JR_ERR_INVALID, "maxpool_bwd: null pointer");
+  const int g = grid_for((int64_t)d->n * d->h * d->w * (d->c / 4));
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_maxpool_bwd<float>, dim3(g), dim3(256), 0, as_stream(stream), *d, argmax,
+                       (const float*)dy, (float*)dx, accumulate);
+  else
+    hipLaunchKernelGGL(k_maxpool_bwd<uint16_t>, dim3(g), dim3(256), 0, as_stream(stream), *d, argmax,
+                       (const uint16_t*)dy, (uint16_t*)dx, accumulate);
+  return check_launch("maxpool_bwd");
+}
+
+JR_API int jr_avgpool3x3s1_fwd(const jr_pool_desc* d, int dtype, const void* x, void* y, void* stream) {
+  int rc = check_pool(d, dtype, false);
+  if (rc) return rc;
+  if (!x || !y) return fail(JR_ERR_INVALID, "avgpool_fwd: null pointer");
+  const int g = grid_for((int64_t)d->n * d->ho * d->wo * (d->c / 4));
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_avgpool_fwd<float>, dim3(g), dim3(256), 0, as_stream(stream), *d, (const float*)x,
+                       (float*)y);
+  else
+    hipLaunchKernelGGL(k_avgpool_fwd<uint16_t>, dim3(g), dim3(256), 0, as_stream(stream), *d,
+                       (const uint16_t*)x, (uint16_t*)y);
+  return check_launch("avgpool_fwd");
+}
+
+JR_API int jr_avgpool3x3s1_bwd(const jr_pool_desc* d, int dtype, const void* dy, void* dx, int accumulate,
+                               void* stream) {
+  int rc = check_pool(d, dtype, false);
+  if (rc) return rc;
+  if (!dy || !dx) return fail(JR_ERR_INVALID, "avgpool_bwd: null pointer");
+  const int g = grid_for((int64_t)d->n * d->h * d->w * (d->c / 4));
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_avgpool_bwd<float>, dim3(g), dim3(256), 0, as_stream(stream), *d, (const float*)dy,
+                       (float*)dx, accumulate);
+  else
+    hipLaunchKernelGGL(k_avgpool_bwd<uint16_t>, dim3(g), dim3(256), 0, as_stream(stream), *d,
+                       (const uint16_t*)dy, (uint16_t*)dx, accumulate);
+  return check_launch("avgpool_bwd");
+}
+
+JR_API int jr_gap_fwd(int dtype, const void* x, int32_t n, int32_t hw, int32_t c, float* y, void* stream) {
+  if (!x || !y || n <= 0 || hw <= 0 || c <= 0 || c % 4) return fail(JR_ERR_INVALID, "gap_fwd: bad arguments");
+  const int g = (int)ceil_div((int64_t)n * (c / 4), 256);
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_gap_fwd<float>, dim3(g), dim3(256), 0, as_stream(stream), (const float*)x, n, hw, c, y);
+  else if (dtype == JR_BF16)
+    hipLaunchKernelGGL(k_gap_fwd<uint16_t>, dim3(g), dim3(256), 0, as_stream(stream), (const uint16_t*)x, n, hw,
+                       c, y);
+  else
+    return fail(JR_ERR_INVALID, "gap_fwd: bad dtype");
+  return check_launch("gap_fwd");
+}
+
+JR_API int jr_gap_bwd(int dtype, const float* dy, int32_t n, int32_t hw, int32_t c, void* dx, void* stream) {
+  if (!dy || !dx || n <= 0 || hw <= 0 || c <= 0 || c % 4) return fail(JR_ERR_INVALID, "gap_bwd: bad arguments");
+  const int g = grid_for((int64_t)n * hw * (c / 4));
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_gap_bwd<float>, dim3(g), dim3(256), 0, as_stream(stream), dy, n, hw, c, (float*)dx);
+  else if (dtype == JR_BF16)
+    hipLaunchKernelGGL(k_gap_bwd<uint16_t>, dim3(g), dim3(256), 0, as_stream(stream), dy, n, hw, c,
+                       (uint16_t*)dx);
+  else
+    return fail(JR_ERR_INVALID, "gap_bwd: bad dtype");
+  return check_launch("gap_bwd");
+}

@@ -1,0 +1,140 @@
+"""ctypes binding of libjr.so (the C-ABI declared in include/jr.h).
+
+This is the only place Python touches the compute library.  Loading is
+strict: if libjr.so is missing or was not built for gfx950 the import fails
+loudly — there is no CPU or PyTorch fallback for any op on the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char_p, c_double, c_float, c_int, c_int32, c_int64,
+                    c_size_t, c_uint8, c_void_p)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("JR_LIB", os.path.join(_HERE, "libjr.so"))
+
+JR_OK = 0
+JR_F32 = 0
+JR_BF16 = 1
+JR_CONV_FWD, JR_CONV_BWD_DATA, JR_CONV_BWD_FILTER = 0, 1, 2
+JR_HEAD_SIGMOID, JR_HEAD_SOFTMAX = 0, 1
+
+
+class JRError(RuntimeError):
+    """A libjr call returned a negative jr_status."""
+
+    def __init__(self, fn: str, status: int, msg: str):
+        super().__init__(f"{fn} failed with status {status}: {msg}")
+        self.status = status
+
+
+class ConvDesc(Structure):
+    _fields_ = [(n, c_int32) for n in (
+        "n", "h", "w", "c_in", "c_out", "kh", "kw", "stride_h", "stride_w", "pad_h", "pad_w",
+        "ho", "wo", "x_c_off", "x_c_stride", "y_c_off", "y_c_stride")]
+
+
+class PoolDesc(Structure):
+    _fields_ = [(n, c_int32) for n in (
+        "n", "h", "w", "c", "ho", "wo", "x_c_off", "x_c_stride", "y_c_off", "y_c_stride")]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "jr_init": (c_int, [c_int]),
+    "jr_last_error": (c_char_p, []),
+    "jr_version": (c_char_p, []),
+    "jr_conv2d_workspace_size": (c_size_t, [POINTER(ConvDesc), c_int, c_int]),
+    "jr_conv2d_fwd": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_size_t, c_void_p]),
+    "jr_conv2d_bwd_data": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                   c_void_p, c_size_t, c_void_p]),
+    "jr_conv2d_bwd_filter": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_size_t, c_void_p]),
+    "jr_bn_workspace_size": (c_size_t, [c_int64, c_int32]),
+    "jr_bn_stats": (c_int, [c_int, c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
+                            c_void_p, c_size_t, c_void_p]),
+    "jr_bn_relu_apply": (c_int, [c_int, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_int32, c_int32, c_void_p]),
+    "jr_bn_relu_bwd": (c_int, [c_int, c_void_p, c_int32, c_int32, c_void_p, c_int64, c_int32,
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_size_t, c_void_p]),
+    "jr_maxpool3x3s2_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p,
+                                    c_void_p]),
+    "jr_maxpool3x3s2_bwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                    c_void_p]),
+    "jr_avgpool3x3s1_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p]),
+    "jr_avgpool3x3s1_bwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "jr_gap_fwd": (c_int, [c_int, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    "jr_gap_bwd": (c_int, [c_int, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    "jr_head_fwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
+                            c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "jr_head_bwd": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
+                            c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "jr_nesterov_update": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
+                                   c_float, c_void_p]),
+    "jr_momentum_update": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
+                                   c_float, c_void_p]),
+    "jr_sgd_update": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
+    "jr_adam_update": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
+                               c_float, c_float, c_float, c_void_p]),
+    "jr_cast_f32_to_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "jr_cast_bf16_to_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "jr_u8_to_f32_scaled": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p]),
+    "jr_brier_accumulate": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "jr_graph_begin": (c_int, [c_void_p]),
+    "jr_graph_end": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "jr_graph_launch": (c_int, [c_void_p, c_void_p]),
+    "jr_graph_destroy": (c_int, [c_void_p]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libjr.so once; raise if it is absent (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libjr.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; "
+            "g.build()'` (hipcc --offload-arch=gfx950); the jr path has no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().jr_last_error().decode(errors="replace")
+
+
+def check(name: str, rc: int) -> None:
+    if rc != JR_OK:
+        raise JRError(name, rc, last_error())
+
+
+def call(name: str, *args) -> int:
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if isinstance(rc, int) and name not in ("jr_conv2d_workspace_size", "jr_bn_workspace_size"):
+        check(name, rc)
+    return rc
+
+
+_inited = set()
+
+
+def init(device: int) -> None:
+    """jr_init: select the device and verify it is gfx950."""
+    if device in _inited:
+        return
+    check("jr_init", load().jr_init(device))
+    _inited.add(device)

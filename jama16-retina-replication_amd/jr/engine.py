@@ -1,0 +1,359 @@
+"""Executor for the Inception-v3 training step / inference on libjr kernels.
+
+The reference runs one `sess.run([global_step, mean_xentropy, train_op,
+update_brier])` per batch (train.py:231-232): forward of the 94 conv2d_bn
+blocks, head + loss, backward, and 190 ApplyMomentum updates.  This module is
+that step, MI355X-native:
+
+* All device memory is planned once per (batch, resolution): one NHWC buffer
+  per block output (concat-free slices), a raw pre-BN buffer per conv (kept
+  for the BN backward), one gradient buffer per activation buffer, a flat fp32
+  parameter / gradient / momentum buffer (so one optimizer launch and one
+  all-reduce bucket walk cover all 190 tensors).  PyTorch tensors are used
+  only as owners of that memory; every op is a libjr C-ABI call.
+* Calls are pre-bound (ctypes function + argument tuple) into call lists, so a
+  step is a flat loop of C calls on one HIP stream, and the whole step can be
+  captured into a HIP graph (jr_graph_*) and replayed.
+* Data parallel: gradients are all-reduced (torch.distributed backend 'nccl' =
+  RCCL over xGMI) in buckets issued during the backward pass, in reverse layer
+  order, so communication overlaps the remaining backward kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _ffi
+from .inception import BN_EPS, ConvNode, Graph, PoolNode, build_inception_v3
+from .init import init_params, param_layout
+
+DTYPES = {"f32": _ffi.JR_F32, "bf16": _ffi.JR_BF16}
+
+
+class Engine:
+    """One model replica on one GPU (one process per GPU)."""
+
+    def __init__(self, batch: int, height: int = 299, width: int = 299, units: int = 1,
+                 device: int | torch.device = 0, dtype: str = "f32", train: bool = True,
+                 optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
+                 head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None):
+        if dtype not in DTYPES:
+            raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
+        if dtype != "f32":
+            raise NotImplementedError("bf16 path: kernels land in a later round")
+        if not torch.cuda.is_available():
+            raise RuntimeError("jr.Engine needs a ROCm GPU (libjr has no CPU path)")
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        _ffi.init(self.device.index or 0)
+        self.lib = _ffi.load()
+        self.g = graph or build_inception_v3(height, width, units)
+        self.batch = batch
+        self.dt = DTYPES[dtype]
+        self.dtype = dtype
+        self.train_mode = train
+        self.optimizer = optimizer
+        self.lr = float(lr)
+        self.momentum = float(momentum)
+        self.head_mode = _ffi.JR_HEAD_SIGMOID if head == "sigmoid" else _ffi.JR_HEAD_SOFTMAX
+        self.units = self.g.units
+        self.stream = torch.cuda.Stream(device=self.device)
+        self._s = ctypes.c_void_p(self.stream.cuda_stream)
+        self.layout, self.nparam = param_layout(self.g.params)
+        self.poffs = {name: (off, size) for name, _, off, size in self.layout}
+        self._alloc()
+        self.load_params(init_params(self.g, seed))
+        self._calls: Dict[int, Tuple[list, list, list]] = {}
+        self._graphs: Dict[int, int] = {}
+        self.bucket_hooks: List[Tuple[int, Callable]] = []
+
+    # ------------------------------------------------------------------ memory
+    def _t(self, n: int, dtype=torch.float32) -> torch.Tensor:
+        return torch.zeros(int(n), dtype=dtype, device=self.device)
+
+    def _alloc(self) -> None:
+        g, B = self.g, self.batch
+        fl = torch.float32
+        self.acts = [self._t(B * b.h * b.w * b.c, fl) for b in g.bufs]
+        self.raw = {n.idx: self._t(B * n.ho * n.wo * n.cout) for n in g.convs}
+        self.stats = self._t(2 * sum(n.cout for n in g.convs))
+        self.mean, self.invstd = {}, {}
+        off = 0
+        for n in g.convs:
+            self.mean[n.idx] = self.stats[off:off + n.cout]
+            self.invstd[n.idx] = self.stats[off + n.cout:off + 2 * n.cout]
+            off += 2 * n.cout
+        self.argmax = {}
+        for i, n in enumerate(g.nodes):
+            if n.kind == "maxpool":
+                self.argmax[i] = self._t(B * n.ho * n.wo * n.c, torch.uint8)
+        feat_c = g.bufs[g.output_buf].c
+        self.feat = self._t(B * feat_c)
+        self.logits = self._t(B * self.units)
+        self.probs = self._t(B * self.units)
+        self.labels = self._t(B * self.units)
+        self.loss = self._t(4)
+        self.params = self._t(self.nparam)
+        if self.train_mode:
+            self.grads = self._t(self.nparam)
+            self.accum = self._t(self.nparam)
+            self.dacts = [self._t(B * b.h * b.w * b.c) if b.id != g.input_buf else None
+                          for b in g.bufs]
+            self.draw = self._t(max(B * n.ho * n.wo * n.cout for n in g.convs))
+            self.dfeat = self._t(B * feat_c)
+        ws = 0
+        for n in g.convs:
+            d = self._conv_desc(n, B)
+            ops = (_ffi.JR_CONV_FWD, _ffi.JR_CONV_BWD_DATA, _ffi.JR_CONV_BWD_FILTER)
+            for op in (ops if self.train_mode else ops[:1]):
+                ws = max(ws, self.lib.jr_conv2d_workspace_size(ctypes.byref(d), op, self.dt))
+            ws = max(ws, self.lib.jr_bn_workspace_size(B * n.ho * n.wo, n.cout))
+        self.ws_bytes = int(ws)
+        self.ws = self._t((self.ws_bytes + 15) // 4 + 4)
+
+    # ------------------------------------------------------------ parameters
+    def load_params(self, flat: np.ndarray) -> None:
+        flat = np.ascontiguousarray(flat, dtype=np.float32)
+        if flat.size != self.nparam:
+            raise ValueError(f"expected {self.nparam} parameters, got {flat.size}")
+        self.params.copy_(torch.from_numpy(flat).to(self.device))
+        if self.train_mode:
+            self.accum.zero_()
+            self.grads.zero_()
+
+    def params_numpy(self) -> np.ndarray:
+        torch.cuda.synchronize(self.device)
+        return self.params.cpu().numpy()
+
+    def _p(self, name: str) -> int:
+        off, _ = self.poffs[name]
+        return self.params.data_ptr() + 4 * off
+
+    def _gp(self, name: str) -> int:
+        off, _ = self.poffs[name]
+        return self.grads.data_ptr() + 4 * off
+
+    # ------------------------------------------------------------ descriptors
+    def _conv_desc(self, n: ConvNode, B: int) -> _ffi.ConvDesc:
+        return _ffi.ConvDesc(B, n.h, n.w, n.cin, n.cout, n.kh, n.kw, n.stride, n.stride,
+                             n.pad_h, n.pad_w, n.ho, n.wo, 0, n.cin, 0, n.cout)
+
+    def _pool_desc(self, n: PoolNode, B: int) -> _ffi.PoolDesc:
+        yb = self.g.bufs[n.y.buf]
+        return _ffi.PoolDesc(B, n.h, n.w, n.c, n.ho, n.wo, 0, n.c, n.y.c_off, yb.c)
+
+    # ------------------------------------------------------------- call lists
+    def _build_calls(self, B: int):
+        """Pre-bound (fn, args, name) lists for forward, backward, update."""
+        if B in self._calls:
+            return self._calls[B]
+        if B > self.batch or B <= 0:
+            raise ValueError(f"batch {B} outside 1..{self.batch}")
+        L, g, s, dt = self.lib, self.g, self._s, self.dt
+        ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
+        keep = []  # keep ctypes structs alive
+        fwd, bwd, opt = [], [], []
+        A = lambda bid: self.acts[bid].data_ptr()  # noqa: E731
+        for i, n in enumerate(g.nodes):
+            if n.kind == "conv":
+                d = self._conv_desc(n, B)
+                keep.append(d)
+                M = B * n.ho * n.wo
+                yb = g.bufs[n.y.buf]
+                fwd.append((L.jr_conv2d_fwd, (ctypes.byref(d), dt, A(n.x), self._p(f"{n.name}/kernel"),
+                                              self.raw[n.idx].data_ptr(), ws, wsb, s), "conv_fwd"))
+                fwd.append((L.jr_bn_stats, (dt, self.raw[n.idx].data_ptr(), M, n.cout, BN_EPS,
+                                            self.mean[n.idx].data_ptr(), self.invstd[n.idx].data_ptr(),
+                                            ws, wsb, s), "bn_stats"))
+                fwd.append((L.jr_bn_relu_apply, (dt, self.raw[n.idx].data_ptr(), M, n.cout,
+                                                 self.mean[n.idx].data_ptr(), self.invstd[n.idx].data_ptr(),
+                                                 self._p(f"batch_normalization_{n.idx + 1}/beta"),
+                                                 A(n.y.buf), n.y.c_off, yb.c, s), "bn_relu"))
+            elif n.kind == "maxpool":
+                d = self._pool_desc(n, B)
+                keep.append(d)
+                fwd.append((L.jr_maxpool3x3s2_fwd, (ctypes.byref(d), dt, A(n.x), A(n.y.buf),
+                                                    self.argmax[i].data_ptr(), s), "maxpool_fwd"))
+            else:
+                d = self._pool_desc(n, B)
+                keep.append(d)
+                fwd.append((L.jr_avgpool3x3s1_fwd, (ctypes.byref(d), dt, A(n.x), A(n.y.buf), s),
+                            "avgpool_fwd"))
+        ob = g.bufs[g.output_buf]
+        fwd.append((L.jr_gap_fwd, (dt, A(g.output_buf), B, ob.h * ob.w, ob.c, self.feat.data_ptr(), s),
+                    "gap_fwd"))
+        fwd.append((L.jr_head_fwd, (self.head_mode, self.feat.data_ptr(), self._p("dense/kernel"),
+                                    self._p("dense/bias"), self.labels.data_ptr(), B, ob.c, self.units,
+                                    self.logits.data_ptr(), self.probs.data_ptr(), self.loss.data_ptr(), s),
+                    "head_fwd"))
+        if self.train_mode:
+            D = lambda bid: self.dacts[bid].data_ptr()  # noqa: E731
+            bwd.append((L.jr_head_bwd, (self.head_mode, self.feat.data_ptr(), self._p("dense/kernel"),
+                                        self.probs.data_ptr(), self.labels.data_ptr(), B, ob.c, self.units,
+                                        self.dfeat.data_ptr(), self._gp("dense/kernel"),
+                                        self._gp("dense/bias"), s), "head_bwd"))
+            bwd.append((L.jr_gap_bwd, (dt, self.dfeat.data_ptr(), B, ob.h * ob.w, ob.c, D(g.output_buf), s),
+                        "gap_bwd"))
+            written = set()
+            for i in range(len(g.nodes) - 1, -1, -1):
+                n = g.nodes[i]
+                yb = g.bufs[n.y.buf]
+                acc = 1 if n.x in written else 0
+                if n.kind == "conv":
+                    d = self._conv_desc(n, B)
+                    keep.append(d)
+                    M = B * n.ho * n.wo
+                    bwd.append((L.jr_bn_relu_bwd, (dt, D(n.y.buf), n.y.c_off, yb.c, self.raw[n.idx].data_ptr(),
+                                                   M, n.cout, self.mean[n.idx].data_ptr(),
+                                                   self.invstd[n.idx].data_ptr(),
+                                                   self._p(f"batch_normalization_{n.idx + 1}/beta"),
+                                                   self.draw.data_ptr(),
+                                                   self._gp(f"batch_normalization_{n.idx + 1}/beta"),
+                                                   ws, wsb, s), "bn_relu_bwd"))
+                    bwd.append((L.jr_conv2d_bwd_filter, (ctypes.byref(d), dt, A(n.x), self.draw.data_ptr(),
+                                                         self._gp(f"{n.name}/kernel"), ws, wsb, s), "conv_wgrad"))
+                    if n.x != g.input_buf:
+                        bwd.append((L.jr_conv2d_bwd_data, (ctypes.byref(d), dt, self.draw.data_ptr(),
+                                                           self._p(f"{n.name}/kernel"), D(n.x), acc, ws, wsb, s),
+                                    "conv_dgrad"))
+                        written.add(n.x)
+                    bwd.append(("param_ready", self.poffs[f"{n.name}/kernel"][0], "hook"))
+                elif n.kind == "maxpool":
+                    d = self._pool_desc(n, B)
+                    keep.append(d)
+                    bwd.append((L.jr_maxpool3x3s2_bwd, (ctypes.byref(d), dt, self.argmax[i].data_ptr(),
+                                                        D(n.y.buf), D(n.x), acc, s), "maxpool_bwd"))
+                    written.add(n.x)
+                else:
+                    d = self._pool_desc(n, B)
+                    keep.append(d)
+                    bwd.append((L.jr_avgpool3x3s1_bwd, (ctypes.byref(d), dt, D(n.y.buf), D(n.x), acc, s),
+                                "avgpool_bwd"))
+                    written.add(n.x)
+            P, G = self.params.data_ptr(), self.grads.data_ptr()
+            if self.optimizer == "nesterov":
+                opt.append((L.jr_nesterov_update, (P, G, self.accum.data_ptr(), self.nparam, self.lr,
+                                                   self.momentum, 1.0, s), "nesterov"))
+            elif self.optimizer == "momentum":
+                opt.append((L.jr_momentum_update, (P, G, self.accum.data_ptr(), self.nparam, self.lr,
+                                                   self.momentum, 1.0, s), "momentum"))
+            elif self.optimizer == "sgd":
+                opt.append((L.jr_sgd_update, (P, G, self.nparam, self.lr, 1.0, s), "sgd"))
+            else:
+                raise ValueError(f"unknown optimizer {self.optimizer}")
+        self._calls[B] = (fwd, bwd, opt, keep)
+        return self._calls[B]
+
+    @staticmethod
+    def _run(calls, hook: Optional[Callable[[int], None]] = None) -> None:
+        for fn, args, name in calls:
+            if fn == "param_ready":
+                if hook is not None:
+                    hook(args)
+                continue
+            rc = fn(*args)
+            if rc:
+                raise _ffi.JRError(name, rc, _ffi.last_error())
+
+    # ------------------------------------------------------------------- data
+    def set_batch(self, images, labels=None, n: Optional[int] = None) -> int:
+        """Copy a batch (NHWC float32, or uint8 to be scaled by 1/255) into the
+        input buffer.  Returns the batch size."""
+        B = int(images.shape[0]) if n is None else n
+        if B > self.batch:
+            raise ValueError(f"batch {B} > planned {self.batch}")
+        ib = self.g.bufs[self.g.input_buf]
+        if tuple(images.shape[1:]) != (ib.h, ib.w, ib.c):
+            raise ValueError(f"images must be [B,{ib.h},{ib.w},{ib.c}] NHWC, got {tuple(images.shape)}")
+        with torch.cuda.stream(self.stream):
+            x = torch.as_tensor(images)
+            if x.dtype == torch.uint8:
+                xd = x.to(self.device, non_blocking=True).reshape(-1)
+                _ffi.check("jr_u8_to_f32_scaled", self.lib.jr_u8_to_f32_scaled(
+                    xd.data_ptr(), self.acts[self.g.input_buf].data_ptr(), self.dt, xd.numel(), self._s))
+                self._keep_u8 = xd
+            else:
+                self.acts[self.g.input_buf][:x.numel()].copy_(
+                    x.to(torch.float32).reshape(-1), non_blocking=True)
+            if labels is not None:
+                y = torch.as_tensor(labels, dtype=torch.float32).reshape(-1)
+                if y.numel() != B * self.units:
+                    raise ValueError("labels must have batch*units elements")
+                self.labels[:y.numel()].copy_(y, non_blocking=True)
+        return B
+
+    # ------------------------------------------------------------------- runs
+    def forward(self, B: Optional[int] = None) -> None:
+        fwd, _, _, _ = self._build_calls(B or self.batch)
+        self._run(fwd)
+
+    def backward(self, B: Optional[int] = None, hook=None) -> None:
+        _, bwd, _, _ = self._build_calls(B or self.batch)
+        self._run(bwd, hook)
+
+    def apply_update(self, B: Optional[int] = None, grad_scale: float = 1.0) -> None:
+        _, _, opt, _ = self._build_calls(B or self.batch)
+        if grad_scale != 1.0:
+            fn, args, name = opt[0]
+            args = list(args)
+            args[-2] = grad_scale
+            opt = [(fn, tuple(args), name)]
+        self._run(opt)
+
+    def train_step(self, B: Optional[int] = None, allreduce=None) -> None:
+        """fwd + bwd (+ bucketed all-reduce) + optimizer, enqueued on self.stream."""
+        B = B or self.batch
+        if allreduce is None:
+            self.forward(B)
+            self.backward(B)
+            self.apply_update(B)
+            return
+        self.forward(B)
+        allreduce.begin(self)
+        self.backward(B, hook=allreduce.param_ready)
+        scale = allreduce.finish(self)
+        self.apply_update(B, grad_scale=scale)
+
+    def capture(self, B: Optional[int] = None) -> None:
+        """Capture fwd+bwd+update for batch B into a HIP graph (single GPU)."""
+        B = B or self.batch
+        fwd, bwd, opt, _ = self._build_calls(B)
+        torch.cuda.synchronize(self.device)
+        _ffi.check("jr_graph_begin", self.lib.jr_graph_begin(self._s))
+        try:
+            self._run(fwd)
+            self._run(bwd)
+            self._run(opt)
+        finally:
+            ex = ctypes.c_void_p()
+            _ffi.check("jr_graph_end", self.lib.jr_graph_end(self._s, ctypes.byref(ex)))
+        self._graphs[B] = ex.value
+
+    def replay(self, B: Optional[int] = None) -> None:
+        B = B or self.batch
+        _ffi.check("jr_graph_launch", self.lib.jr_graph_launch(ctypes.c_void_p(self._graphs[B]), self._s))
+
+    def synchronize(self) -> None:
+        self.stream.synchronize()
+
+    def loss_value(self) -> float:
+        self.synchronize()
+        return float(self.loss[0].item())
+
+    def predictions(self, B: Optional[int] = None) -> np.ndarray:
+        B = B or self.batch
+        self.synchronize()
+        return self.probs[:B * self.units].cpu().numpy().reshape(B, self.units)
+
+    def close(self) -> None:
+        for ex in self._graphs.values():
+            self.lib.jr_graph_destroy(ctypes.c_void_p(ex))
+        self._graphs.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

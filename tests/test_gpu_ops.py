@@ -1,0 +1,269 @@
+"""Per-op parity: libjr HIP kernels (through the C-ABI) vs the numpy fp64
+oracle (oracle/tf_ops.py) on seeded inputs.  fp32 tolerances are stated per
+test; integer/index work (argmax routing) is compared exactly."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import tf_ops as R
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _lib():
+    from jr import _ffi
+    _ffi.init(0)
+    return _ffi
+
+
+def dev(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a)).to("cuda", dtype=dtype)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def relerr(got, ref):
+    ref = np.asarray(ref, np.float64)
+    return float(np.max(np.abs(got - ref)) / max(np.max(np.abs(ref)), 1e-30))
+
+
+CONV_CASES = [
+    # n, h, w, cin, cout, kh, kw, stride, padding
+    (2, 35, 35, 192, 64, 1, 1, 1, "same"),
+    (2, 35, 35, 48, 64, 5, 5, 1, "same"),
+    (2, 17, 17, 128, 192, 1, 7, 1, "same"),
+    (2, 17, 17, 160, 160, 7, 1, 1, "same"),
+    (2, 35, 35, 288, 384, 3, 3, 2, "valid"),
+    (3, 17, 17, 192, 320, 3, 3, 2, "valid"),
+    (2, 8, 8, 448, 384, 3, 3, 1, "same"),
+    (2, 8, 8, 384, 384, 1, 3, 1, "same"),
+    (2, 73, 73, 80, 192, 3, 3, 1, "valid"),
+    (2, 37, 37, 3, 32, 3, 3, 2, "valid"),     # conv1 (scalar A path)
+    (1, 29, 31, 32, 48, 3, 3, 1, "same"),     # ragged M / N tails
+]
+
+
+def _desc(ffi, n, h, w, cin, cout, kh, kw, s, pad, x_off=0, x_stride=None, y_off=0, y_stride=None):
+    ph, pw = ((kh - 1) // 2, (kw - 1) // 2) if pad == "same" else (0, 0)
+    ho, wo = (h + 2 * ph - kh) // s + 1, (w + 2 * pw - kw) // s + 1
+    return ffi.ConvDesc(n, h, w, cin, cout, kh, kw, s, s, ph, pw, ho, wo, x_off, x_stride or cin,
+                        y_off, y_stride or cout), ho, wo
+
+
+def _ws(ffi, d, op):
+    b = ffi.load().jr_conv2d_workspace_size(ctypes.byref(d), op, 0)
+    return torch.zeros(max(b // 4, 1) + 4, device="cuda"), b
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case):
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, cin, cout, kh, kw, s, pad = case
+    rng = np.random.default_rng(hash(case) % 2**31)
+    x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
+    wt = (rng.standard_normal((kh, kw, cin, cout)) / np.sqrt(kh * kw * cin)).astype(np.float32)
+    d, ho, wo = _desc(ffi, n, h, w, cin, cout, kh, kw, s, pad)
+    ref = R.conv2d(x, wt, s, pad)
+    X, W = dev(x), dev(wt)
+    Y = torch.zeros(n * ho * wo * cout, device="cuda")
+    ws, wsb = _ws(ffi, d, 0)
+    ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), 0, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
+                                     ws.data_ptr(), wsb, None))
+    got = host(Y).reshape(ref.shape)
+    assert relerr(got, ref) < 5e-6, relerr(got, ref)
+
+    dy = rng.standard_normal(ref.shape).astype(np.float32)
+    DY = dev(dy)
+    if cin % 4 == 0 and cout % 16 == 0:
+        ref_dx = R.conv2d_bwd_data(dy, wt, x.shape, s, pad)
+        DX = torch.zeros(x.size, device="cuda")
+        ws, wsb = _ws(ffi, d, 1)
+        ffi.check("dgrad", L.jr_conv2d_bwd_data(ctypes.byref(d), 0, DY.data_ptr(), W.data_ptr(), DX.data_ptr(),
+                                                0, ws.data_ptr(), wsb, None))
+        got = host(DX).reshape(x.shape)
+        assert relerr(got, ref_dx) < 5e-6, relerr(got, ref_dx)
+        # accumulate = 1 adds into the existing gradient
+        ffi.check("dgrad acc", L.jr_conv2d_bwd_data(ctypes.byref(d), 0, DY.data_ptr(), W.data_ptr(),
+                                                    DX.data_ptr(), 1, ws.data_ptr(), wsb, None))
+        got = host(DX).reshape(x.shape)
+        assert relerr(got, 2 * ref_dx) < 5e-6
+    ref_dw = R.conv2d_bwd_filter(x, dy, wt.shape, s, pad)
+    DW = torch.zeros(wt.size, device="cuda")
+    ws, wsb = _ws(ffi, d, 2)
+    ffi.check("wgrad", L.jr_conv2d_bwd_filter(ctypes.byref(d), 0, X.data_ptr(), DY.data_ptr(), DW.data_ptr(),
+                                              ws.data_ptr(), wsb, None))
+    got = host(DW).reshape(wt.shape)
+    assert relerr(got, ref_dw) < 1e-5, relerr(got, ref_dw)
+
+
+def test_conv_channel_slices():
+    """Input read from / output written to channel slices of wider buffers
+    (concat-free Inception-block writes)."""
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, cin, cout = 2, 9, 9, 32, 48
+    rng = np.random.default_rng(5)
+    big_x = rng.standard_normal((n, h, w, 80)).astype(np.float32)
+    x = big_x[..., 16:48]
+    wt = rng.standard_normal((3, 3, cin, cout)).astype(np.float32) * 0.1
+    d, ho, wo = _desc(ffi, n, h, w, cin, cout, 3, 3, 1, "same", x_off=16, x_stride=80, y_off=64, y_stride=128)
+    ref = R.conv2d(x, wt, 1, "same")
+    Y = torch.full((n * ho * wo * 128,), 7.0, device="cuda")
+    ws, wsb = _ws(ffi, d, 0)
+    ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), 0, dev(big_x).data_ptr(), dev(wt).data_ptr(), Y.data_ptr(),
+                                     ws.data_ptr(), wsb, None))
+    got = host(Y).reshape(n, ho, wo, 128)
+    assert relerr(got[..., 64:112], ref) < 2e-6
+    assert np.all(got[..., :64] == 7.0) and np.all(got[..., 112:] == 7.0)
+
+
+def test_conv_rejects_bad_geometry():
+    ffi = _lib()
+    L = ffi.load()
+    d, _, _ = _desc(ffi, 1, 8, 8, 16, 16, 3, 3, 1, "same")
+    d.ho = 9
+    rc = L.jr_conv2d_fwd(ctypes.byref(d), 0, 1, 1, 1, None, 0, None)
+    assert rc == -1 and "ho/wo" in ffi.last_error()
+
+
+@pytest.mark.parametrize("m,c", [(2 * 35 * 35, 64), (3 * 17 * 17, 192), (64 * 8 * 8, 448), (5, 48), (100003, 80)])
+def test_bn_relu_fwd_bwd(m, c):
+    ffi = _lib()
+    L = ffi.load()
+    rng = np.random.default_rng(m + c)
+    x = (rng.standard_normal((m, c)) * 3 + rng.standard_normal(c) * 2).astype(np.float32)
+    beta = (rng.standard_normal(c) * 0.5).astype(np.float32)
+    dy = rng.standard_normal((m, c)).astype(np.float32)
+    y_ref, mean_ref, inv_ref = R.bn_relu_fwd(x, beta)
+    X, BETA = dev(x), dev(beta)
+    MEAN, INV = torch.zeros(c, device="cuda"), torch.zeros(c, device="cuda")
+    wsb = L.jr_bn_workspace_size(m, c)
+    ws = torch.zeros(wsb // 4 + 4, device="cuda")
+    ffi.check("stats", L.jr_bn_stats(0, X.data_ptr(), m, c, 1e-3, MEAN.data_ptr(), INV.data_ptr(),
+                                     ws.data_ptr(), wsb, None))
+    assert relerr(host(MEAN), mean_ref) < 1e-6
+    assert relerr(host(INV), inv_ref) < 1e-6
+    # write into a channel slice of a wider buffer
+    Y = torch.zeros(m * (c + 16), device="cuda")
+    ffi.check("apply", L.jr_bn_relu_apply(0, X.data_ptr(), m, c, MEAN.data_ptr(), INV.data_ptr(), BETA.data_ptr(),
+                                          Y.data_ptr(), 16, c + 16, None))
+    got = host(Y).reshape(m, c + 16)
+    assert np.max(np.abs(got[:, 16:] - y_ref)) < 2e-5 * max(1.0, np.abs(y_ref).max())
+    assert np.all(got[:, :16] == 0)
+    dx_ref, db_ref = R.bn_relu_bwd(dy, x, beta, mask=got[:, 16:] > 0)
+    DYb = np.zeros((m, c + 8), np.float32)
+    DYb[:, 8:] = dy
+    DX, DB = torch.zeros(m * c, device="cuda"), torch.zeros(c, device="cuda")
+    ffi.check("bwd", L.jr_bn_relu_bwd(0, dev(DYb).data_ptr(), 8, c + 8, X.data_ptr(), m, c, MEAN.data_ptr(),
+                                      INV.data_ptr(), BETA.data_ptr(), DX.data_ptr(), DB.data_ptr(), ws.data_ptr(),
+                                      wsb, None))
+    assert relerr(host(DB), db_ref) < 1e-5
+    assert relerr(host(DX).reshape(m, c), dx_ref) < 1e-4
+
+
+@pytest.mark.parametrize("shape", [(2, 147, 147, 64), (2, 35, 35, 288), (3, 17, 17, 768), (1, 9, 10, 8)])
+def test_maxpool(shape):
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, c = shape
+    rng = np.random.default_rng(sum(shape))
+    x = np.maximum(rng.standard_normal(shape), 0).astype(np.float32)   # post-ReLU input (ties at 0)
+    y_ref, am_ref = R.maxpool3x3s2(x)
+    ho, wo = y_ref.shape[1:3]
+    d = ffi.PoolDesc(n, h, w, c, ho, wo, 0, c, 0, c)
+    X = dev(x)
+    Y = torch.zeros(y_ref.size, device="cuda")
+    AM = torch.zeros(y_ref.size, dtype=torch.uint8, device="cuda")
+    ffi.check("mp fwd", L.jr_maxpool3x3s2_fwd(ctypes.byref(d), 0, X.data_ptr(), Y.data_ptr(), AM.data_ptr(), None))
+    assert np.array_equal(host(Y).reshape(y_ref.shape), y_ref.astype(np.float32))
+    assert np.array_equal(host(AM).reshape(y_ref.shape), am_ref)
+    dy = rng.standard_normal(y_ref.shape).astype(np.float32)
+    dx_ref = R.maxpool3x3s2_bwd(dy, am_ref, x.shape)
+    DX = torch.ones(x.size, device="cuda")
+    ffi.check("mp bwd", L.jr_maxpool3x3s2_bwd(ctypes.byref(d), 0, AM.data_ptr(), dev(dy).data_ptr(), DX.data_ptr(),
+                                              1, None))
+    assert np.allclose(host(DX).reshape(x.shape), dx_ref + 1.0, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape", [(2, 35, 35, 192), (2, 17, 17, 768), (2, 8, 8, 1280), (1, 3, 5, 4)])
+def test_avgpool(shape):
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, c = shape
+    rng = np.random.default_rng(sum(shape) + 1)
+    x = rng.standard_normal(shape).astype(np.float32)
+    y_ref = R.avgpool3x3s1_same(x)
+    d = ffi.PoolDesc(n, h, w, c, h, w, 0, c, 0, c)
+    Y = torch.zeros(x.size, device="cuda")
+    ffi.check("ap fwd", L.jr_avgpool3x3s1_fwd(ctypes.byref(d), 0, dev(x).data_ptr(), Y.data_ptr(), None))
+    assert relerr(host(Y).reshape(shape), y_ref) < 1e-6
+    dy = rng.standard_normal(shape).astype(np.float32)
+    dx_ref = R.avgpool3x3s1_same_bwd(dy)
+    DX = torch.zeros(x.size, device="cuda")
+    ffi.check("ap bwd", L.jr_avgpool3x3s1_bwd(ctypes.byref(d), 0, dev(dy).data_ptr(), DX.data_ptr(), 0, None))
+    assert relerr(host(DX).reshape(shape), dx_ref) < 1e-6
+
+
+def test_gap_head_loss():
+    ffi = _lib()
+    L = ffi.load()
+    rng = np.random.default_rng(11)
+    n, hw, c = 5, 64, 2048
+    x = np.maximum(rng.standard_normal((n, hw, c)), 0).astype(np.float32)
+    W = (rng.standard_normal((c, 1)) * 0.05).astype(np.float32)
+    b = np.array([0.1], np.float32)
+    y = np.array([[0], [1], [1], [0], [1]], np.float32)
+    F = torch.zeros(n * c, device="cuda")
+    ffi.check("gap", L.jr_gap_fwd(0, dev(x).data_ptr(), n, hw, c, F.data_ptr(), None))
+    f_ref = R.global_avg_pool(x.reshape(n, 8, 8, c))
+    assert relerr(host(F).reshape(n, c), f_ref) < 1e-6
+    LOG, PR, LOSS = (torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda"), torch.zeros(1, device="cuda"))
+    Wd, Y = dev(W), dev(y)
+    ffi.check("head", L.jr_head_fwd(0, F.data_ptr(), Wd.data_ptr(), dev(b).data_ptr(), Y.data_ptr(), n, c, 1,
+                                    LOG.data_ptr(), PR.data_ptr(), LOSS.data_ptr(), None))
+    z_ref = R.dense(f_ref, W, b)
+    assert relerr(host(LOG).reshape(n, 1), z_ref) < 1e-5
+    assert np.allclose(host(PR).reshape(n, 1), R.sigmoid(z_ref), atol=1e-6)
+    assert abs(host(LOSS)[0] - R.sigmoid_xent_mean(z_ref, y)) < 1e-6
+    DF, DW, DB = torch.zeros(n * c, device="cuda"), torch.zeros(c, device="cuda"), torch.zeros(1, device="cuda")
+    ffi.check("head bwd", L.jr_head_bwd(0, F.data_ptr(), Wd.data_ptr(), PR.data_ptr(), Y.data_ptr(), n, c, 1,
+                                        DF.data_ptr(), DW.data_ptr(), DB.data_ptr(), None))
+    dz = R.sigmoid_xent_grad(z_ref, y)
+    assert relerr(host(DW).reshape(c, 1), f_ref.T @ dz) < 1e-5
+    assert relerr(host(DB), dz.sum(0)) < 1e-5
+    assert relerr(host(DF).reshape(n, c), dz @ W.T) < 1e-5
+    DX = torch.zeros(n * hw * c, device="cuda")
+    ffi.check("gap bwd", L.jr_gap_bwd(0, DF.data_ptr(), n, hw, c, DX.data_ptr(), None))
+    assert relerr(host(DX).reshape(n, hw, c), np.repeat((dz @ W.T)[:, None, :] / hw, hw, axis=1)) < 1e-5
+
+
+def test_optimizers():
+    ffi = _lib()
+    L = ffi.load()
+    rng = np.random.default_rng(3)
+    n = 1003
+    w, g, a = (rng.standard_normal(n).astype(np.float32) for _ in range(3))
+    W, G, A = dev(w), dev(g), dev(a)
+    ffi.check("nest", L.jr_nesterov_update(W.data_ptr(), G.data_ptr(), A.data_ptr(), n, 3e-3, 0.9, 1.0, None))
+    w_ref, a_ref = R.nesterov(w.astype(np.float64), g, a, 3e-3, 0.9)
+    assert np.allclose(host(W), w_ref, rtol=1e-6, atol=1e-7)
+    assert np.allclose(host(A), a_ref, rtol=1e-6, atol=1e-7)
+    W2 = dev(w)
+    ffi.check("sgd", L.jr_sgd_update(W2.data_ptr(), G.data_ptr(), n, 3e-3, 1.0, None))
+    assert np.allclose(host(W2), R.sgd(w.astype(np.float64), g, 3e-3), rtol=1e-6, atol=1e-7)
+
+
+def test_u8_scale_is_tf_convert_image_dtype():
+    ffi = _lib()
+    L = ffi.load()
+    u8 = np.arange(256, dtype=np.uint8)
+    out = torch.zeros(256, device="cuda")
+    ffi.check("u8", L.jr_u8_to_f32_scaled(dev(u8, torch.uint8).data_ptr(), out.data_ptr(), 0, 256, None))
+    assert np.array_equal(host(out), R.convert_image_dtype_u8(u8))
