@@ -477,10 +477,10 @@ static int validate(const jr_conv_desc* d) {
     return fail(JR_ERR_INVALID, "conv: input channel slice out of range");
   if (d->y_c_off < 0 || d->y_c_off + d->c_out > d->y_c_stride)
     return fail(JR_ERR_INVALID, "conv: output channel slice out of range");
-  if (d->c_out % 4 != 0 || d->x_c_stride % 4 != 0 || d->y_c_stride % 4 != 0 || d->y_c_off % 4 != 0)
-    return fail(JR_ERR_INVALID, "conv: c_out, strides and output offset must be multiples of 4");
-  if (d->c_in % 16 == 0 && d->x_c_off % 4 != 0)
-    return fail(JR_ERR_INVALID, "conv: input offset must be a multiple of 4");
+  if (d->c_out % 4 != 0 || d->y_c_stride % 4 != 0 || d->y_c_off % 4 != 0)
+    return fail(JR_ERR_INVALID, "conv: c_out, output stride and output offset must be multiples of 4");
+  if (d->c_in % 4 == 0 && (d->x_c_off % 4 != 0 || d->x_c_stride % 4 != 0))
+    return fail(JR_ERR_INVALID, "conv: input offset/stride must be multiples of 4 when c_in is");
   const long long big = (long long)d->n * d->h * d->w * d->x_c_stride;
   const long long bigo = (long long)d->n * d->ho * d->wo * d->y_c_stride;
   if (big >= (1LL << 31) * 4 || bigo >= (1LL << 31) * 4)

@@ -28,6 +28,7 @@ class InceptionV3Ref:
         self.P = {k: torch.tensor(np.asarray(v), dtype=dtype, requires_grad=requires_grad)
                   for k, v in params.items()}
         self._k = 0
+        self.record = None   # set to [] to keep every conv2d_bn output (and its grad)
 
     # keras_applications.inception_v3.conv2d_bn
     def conv2d_bn(self, x, filters, num_row, num_col, padding="same", strides=(1, 1)):
@@ -40,7 +41,12 @@ class InceptionV3Ref:
         mean = y.mean(dim=(0, 2, 3), keepdim=True)
         var = ((y - mean) ** 2).mean(dim=(0, 2, 3), keepdim=True)      # biased
         y = (y - mean) / torch.sqrt(var + EPS) + beta.view(1, -1, 1, 1)
-        return F.relu(y)
+        y = F.relu(y)
+        if self.record is not None:          # debugging aid: keep every block output
+            if y.requires_grad:
+                y.retain_grad()
+            self.record.append(y)
+        return y
 
     @staticmethod
     def maxpool(x):

@@ -19,8 +19,23 @@ def _lib():
     return _ffi
 
 
+_KEEP = []
+
+
+@pytest.fixture(autouse=True)
+def _keep_alive():
+    """Device copies made by dev() live until the test ends: a temporary whose
+    data_ptr() is passed to a kernel must not return to the caching allocator
+    (and be handed to the next allocation) before the kernel has run."""
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
+
+
 def dev(a, dtype=torch.float32):
-    return torch.as_tensor(np.ascontiguousarray(a)).to("cuda", dtype=dtype)
+    t = torch.as_tensor(np.ascontiguousarray(a)).to("cuda", dtype=dtype)
+    _KEEP.append(t)
+    return t
 
 
 def host(t):

@@ -1,0 +1,30 @@
+"""Debug: per-conv forward outputs and dL/dy of jr.Engine vs the fp64 oracle."""
+import sys, os
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "jama16-retina-replication_amd"))
+import numpy as np, torch
+from jr.engine import Engine
+from jr.init import unflatten
+from jr import synth
+from oracle.inception_ref import InceptionV3Ref
+
+res, B = int(sys.argv[1]) if len(sys.argv) > 1 else 107, 3
+eng = Engine(B, res, res, seed=1)
+imgs = synth.fundus_batch(0, B, res)
+y = np.array([[1.0], [0.0], [1.0]][:B], np.float32)
+eng.set_batch(imgs, y)
+ref = InceptionV3Ref(unflatten(eng.g, eng.params_numpy()), torch.float64)
+ref.record = []
+ref.train_step(imgs.astype(np.float32) * np.float32(1 / 255), y, {})
+eng.forward(); eng.backward(); eng.synchronize()
+acts = [a.cpu().numpy() for a in eng.acts]
+dacts = [None if d is None else d.cpu().numpy() for d in eng.dacts]
+for n, yo in zip(eng.g.convs, ref.record):
+    bf = eng.g.bufs[n.y.buf]
+    a = acts[n.y.buf].reshape(B, bf.h, bf.w, bf.c)[..., n.y.c_off:n.y.c_off + n.cout]
+    r = yo.detach().permute(0, 2, 3, 1).numpy()
+    fe = np.max(np.abs(a - r)) / max(np.abs(r).max(), 1e-9)
+    d = dacts[n.y.buf].reshape(B, bf.h, bf.w, bf.c)[..., n.y.c_off:n.y.c_off + n.cout]
+    rg = yo.grad.permute(0, 2, 3, 1).numpy()
+    ge = np.linalg.norm(d - rg) / max(np.linalg.norm(rg), 1e-30)
+    print(f"conv{n.idx+1:3d} {n.kh}x{n.kw}/{n.stride} {n.h}x{n.w}x{n.cin}->{n.cout} buf={bf.name}@{n.y.c_off} fwd_rel={fe:.2e} dy_rel={ge:.2e}")
