@@ -63,6 +63,8 @@ static ChunkGeom chunk_geom(int64_t m, int c) {
   const int tpr = c / 4;                       // threads per row
   const int rpp = tpr <= 256 ? 256 / tpr : 1;  // rows per pass
   if (rpc < rpp) rpc = rpp;
+  const int64_t min_rows = ceil_div(16384, c);  // >= 64 KiB of fp32 input per block
+  if (rpc < min_rows) rpc = min_rows;
   g.rows_per_chunk = (int)rpc;
   g.nchunks = (int)ceil_div(m, rpc);
   return g;
@@ -137,18 +139,30 @@ __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, cons
   }
 }
 
-// Fixed-order combine of the chunk partials.
+// Fixed-order combine of the chunk partials: block = 16 channels x 16 chunk
+// lanes; lane ty sums chunks ty, ty+16, ... then lane sums are added in lane
+// order (deterministic, independent of timing).
 // MODE 0: mean, invstd.   MODE 1: k1 = sum dy'/m, k2 = sum dy'xhat/m, dbeta.
 template <int MODE>
-__global__ void k_bn_finalize(const double* __restrict__ part, int nchunks, int c, int64_t m, float eps,
-                              float* out0, float* out1, float* dbeta) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= c) return;
+__global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ part, int nchunks, int c,
+                                                     int64_t m, float eps, float* out0, float* out1,
+                                                     float* dbeta) {
+  __shared__ double red[2][16][17];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int k = blockIdx.x * 16 + tx;
   double s0 = 0, s1 = 0;
-  for (int i = 0; i < nchunks; ++i) {
-    s0 += part[(int64_t)i * 2 * c + k];
-    s1 += part[(int64_t)i * 2 * c + c + k];
+  if (k < c) {
+    for (int i = ty; i < nchunks; i += 16) {
+      s0 += part[(int64_t)i * 2 * c + k];
+      s1 += part[(int64_t)i * 2 * c + c + k];
+    }
   }
+  red[0][ty][tx] = s0;
+  red[1][ty][tx] = s1;
+  __syncthreads();
+  if (ty != 0 || k >= c) return;
+  s0 = 0; s1 = 0;
+  for (int j = 0; j < 16; ++j) { s0 += red[0][j][tx]; s1 += red[1][j][tx]; }
   const double inv_m = 1.0 / (double)m;
   if (MODE == 0) {
     const double mu = s0 * inv_m;
@@ -265,7 +279,7 @@ JR_API int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps
                        part);
   rc = check_launch("bn_stats reduce");
   if (rc) return rc;
-  hipLaunchKernelGGL((k_bn_finalize<0>), dim3((int)ceil_div(c, 256)), dim3(256), 0, s, part, g.nchunks, c, m,
+  hipLaunchKernelGGL((k_bn_finalize<0>), dim3((int)ceil_div(c, 16)), dim3(256), 0, s, part, g.nchunks, c, m,
                      eps, mean, invstd, (float*)nullptr);
   return check_launch("bn_stats finalize");
 }
@@ -314,7 +328,7 @@ JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t d
                        beta, part);
   rc = check_launch("bn_bwd reduce");
   if (rc) return rc;
-  hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 256)), dim3(256), 0, s, part, g.nchunks, c, m,
+  hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 16)), dim3(256), 0, s, part, g.nchunks, c, m,
                      0.f, k1, k2, dbeta);
   rc = check_launch("bn_bwd finalize");
   if (rc) return rc;

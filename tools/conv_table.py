@@ -1,0 +1,41 @@
+"""Map k_conv_f32 dispatches of a rocprofv3 kernel trace to (layer, op) and
+print per-call achieved TFLOP/s for the last training step in the trace."""
+import csv, sys, os
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "jama16-retina-replication_amd"))
+from jr.inception import build_inception_v3
+
+trace = sys.argv[1]
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 64
+rows = [r for r in csv.DictReader(open(trace)) if r["Kind"] == "KERNEL_DISPATCH"]
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+g = build_inception_v3()
+seq = [(n, "fwd") for n in g.convs]
+for n in reversed(g.convs):
+    seq.append((n, "wgrad"))
+    if n.idx != 0:
+        seq.append((n, "dgrad"))
+conv = []
+i = 0
+while i < len(rows):
+    r = rows[i]
+    if "k_conv_f32" in r["Kernel_Name"]:
+        t = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        j = i + 1
+        if j < len(rows) and "splitk_reduce" in rows[j]["Kernel_Name"]:
+            t2 = int(rows[j]["End_Timestamp"]) - int(rows[j]["Start_Timestamp"])
+        else:
+            t2 = 0
+        conv.append((r, t, t2))
+    i += 1
+last = conv[-len(seq):]
+tot_t = 0; tot_f = 0
+out = []
+for (n, op), (r, t, t2) in zip(seq, last):
+    f = 2 * n.macs_per_image() * B
+    tot_t += t + t2; tot_f += f
+    name = r["Kernel_Name"]; cfg = name[name.index("<"):name.index(">") + 1]
+    out.append((t + t2, f"{n.name:10s} {op:5s} {n.kh}x{n.kw}/{n.stride} {n.h:3d}x{n.w:<3d} {n.cin:4d}->{n.cout:4d} "
+                f"{cfg:24s} grid={r['Grid_Size_X']:>7s}x{r['Grid_Size_Z']:<4s} {t/1e3:8.1f}+{t2/1e3:6.1f}us {f/(t+t2)/1e3:7.1f} TF/s"))
+for t, s in sorted(out, reverse=True)[:int(sys.argv[3]) if len(sys.argv) > 3 else 40]:
+    print(s)
+print(f"total conv {tot_t/1e6:.2f} ms, {tot_f/tot_t/1e3:.1f} TF/s")

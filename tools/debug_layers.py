@@ -8,18 +8,22 @@ from jr.init import unflatten
 from jr import synth
 from oracle.inception_ref import InceptionV3Ref
 
-res, B = int(sys.argv[1]) if len(sys.argv) > 1 else 107, 3
+res = int(sys.argv[1]) if len(sys.argv) > 1 else 107
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 eng = Engine(B, res, res, seed=1)
 imgs = synth.fundus_batch(0, B, res)
-y = np.array([[1.0], [0.0], [1.0]][:B], np.float32)
+y = synth.labels(0, B)
 eng.set_batch(imgs, y)
 ref = InceptionV3Ref(unflatten(eng.g, eng.params_numpy()), torch.float64)
 ref.record = []
 ref.train_step(imgs.astype(np.float32) * np.float32(1 / 255), y, {})
+ref32 = InceptionV3Ref(unflatten(eng.g, eng.params_numpy()), torch.float32)
+ref32.record = []
+ref32.train_step(imgs.astype(np.float32) * np.float32(1 / 255), y, {})
 eng.forward(); eng.backward(); eng.synchronize()
 acts = [a.cpu().numpy() for a in eng.acts]
 dacts = [None if d is None else d.cpu().numpy() for d in eng.dacts]
-for n, yo in zip(eng.g.convs, ref.record):
+for n, yo, y32 in zip(eng.g.convs, ref.record, ref32.record):
     bf = eng.g.bufs[n.y.buf]
     a = acts[n.y.buf].reshape(B, bf.h, bf.w, bf.c)[..., n.y.c_off:n.y.c_off + n.cout]
     r = yo.detach().permute(0, 2, 3, 1).numpy()
@@ -27,4 +31,7 @@ for n, yo in zip(eng.g.convs, ref.record):
     d = dacts[n.y.buf].reshape(B, bf.h, bf.w, bf.c)[..., n.y.c_off:n.y.c_off + n.cout]
     rg = yo.grad.permute(0, 2, 3, 1).numpy()
     ge = np.linalg.norm(d - rg) / max(np.linalg.norm(rg), 1e-30)
-    print(f"conv{n.idx+1:3d} {n.kh}x{n.kw}/{n.stride} {n.h}x{n.w}x{n.cin}->{n.cout} buf={bf.name}@{n.y.c_off} fwd_rel={fe:.2e} dy_rel={ge:.2e}")
+    r32 = y32.grad.permute(0, 2, 3, 1).double().numpy()
+    ge32 = np.linalg.norm(r32 - rg) / max(np.linalg.norm(rg), 1e-30)
+    fe32 = np.max(np.abs(y32.detach().permute(0, 2, 3, 1).double().numpy() - r)) / max(np.abs(r).max(), 1e-9)
+    print(f"[cpu32 fwd {fe32:.2e} dy {ge32:.2e}] conv{n.idx+1:3d} {n.kh}x{n.kw}/{n.stride} {n.h}x{n.w}x{n.cin}->{n.cout} buf={bf.name}@{n.y.c_off} fwd_rel={fe:.2e} dy_rel={ge:.2e}")
