@@ -79,6 +79,11 @@ const char* jr_version(void);
 /* ---- convolution (train.py:129-130 -> Keras Conv2D -> TF Conv2D,
  *      Conv2DBackpropInput, Conv2DBackpropFilter created by .minimize at
  *      train.py:150-153) ----------------------------------------------- */
+/* c_out must be a multiple of 16.  c_in % 4 != 0 (the 3-channel image of
+ * conv1) is supported for fwd / bwd_filter by virtual padding to
+ * c4 = round_up(c_in, 4): the input buffer must hold c4 channels per pixel
+ * (x_c_off + c4 <= x_c_stride) and channels [c_in, c4) must be finite
+ * (zero); the kernel tensor stays [kh][kw][c_in][c_out]. */
 size_t jr_conv2d_workspace_size(const jr_conv_desc* d, int op, int dtype);
 /* y[.., y_c_off + co] = sum x * w   (raw conv output, no bias) */
 int jr_conv2d_fwd(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y,
@@ -89,6 +94,18 @@ int jr_conv2d_bwd_data(const jr_conv_desc* d, int dtype, const void* dy, const v
 /* dw[kh][kw][ci][co] = sum x * dy  (fp32 output for both dtypes) */
 int jr_conv2d_bwd_filter(const jr_conv_desc* d, int dtype, const void* x, const void* dy, float* dw,
                          void* ws, size_t ws_bytes, void* stream);
+
+/* Time every candidate tile configuration of this op on the given buffers
+ * (the output buffer is overwritten; host-synchronising) and cache the
+ * fastest for later calls with the same geometry in this process.  Call
+ * once per layer at plan time, outside graph capture. */
+int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const void* a, const void* b, void* c,
+                       void* ws, size_t ws_bytes, void* stream);
+/* Tile configuration the next call would use (DGRAD: per stride phase),
+ * and an explicit override (reproducibility, tests). */
+int jr_conv2d_get_config(const jr_conv_desc* d, int op, int phase);
+int jr_conv2d_set_config(const jr_conv_desc* d, int op, int phase, int cfg);
+int jr_conv2d_num_configs(void);
 
 /* ---- BatchNormalization(scale=False, eps) + ReLU, training-mode batch
  *      statistics (Keras conv2d_bn; App. C Q1: always batch stats) ----- */
@@ -153,6 +170,11 @@ int jr_cast_bf16_to_f32(const void* src, float* dst, int64_t n, void* stream);
 /* uint8 HWC images -> f32 * f32(1/255) (tf.image.convert_image_dtype,
  * lib/dataset.py:20-21) */
 int jr_u8_to_f32_scaled(const uint8_t* src, void* dst, int dtype, int64_t n, void* stream);
+/* uint8 [pixels][c] images -> dst [pixels][dst_stride] of f32(x) * f32(1/255),
+ * channels [c, dst_stride) set to 0 (the conv1 input is kept 4 channels
+ * wide, see jr_conv2d_fwd on c_in % 4 != 0). */
+int jr_image_u8_to_nhwc(const uint8_t* src, void* dst, int dtype, int64_t pixels, int32_t c,
+                        int32_t dst_stride, void* stream);
 /* acc[0] += sum (p - y)^2, acc[1] += n   (tf.metrics.mean_squared_error,
  * train.py:175-177) */
 int jr_brier_accumulate(const float* probs, const float* labels, int32_t n, double* acc, void* stream);

@@ -8,18 +8,36 @@
 // One GEMM  C[M][N] = sum_k A[m][k] * B[k][n]  per op, activations NHWC,
 // kernels HWIO:
 //   FWD    m = output pixel (b,ho,wo)  n = co  k = (r,c,ci)   A = x gather,  B = W
-//   DGRAD  m = input pixel  (b,h,w)    n = ci  k = (r,c,co)   A = dy gather, B = W^T(ci,co)
+//   DGRAD  m = input pixel of one stride phase (b,u,v)  n = ci  k = (a,b,co)
+//          A = dy gather, B = W^T; a stride-s conv is split into s*s phase
+//          GEMMs (input pixels with (h%s, w%s) fixed see only the taps
+//          r = r0 + s*a), so no MAC multiplies a structural zero
 //   WGRAD  m = (r,c,ci)                n = co  k = pixel      A = x gather^T, B = dy
-// Tiles are staged through LDS in a k-major image ([BK][BM], [BK][BN]) so
-// every MFMA operand is one conflict-free ds_read_b32 per lane; k-contiguous
-// global operands are transposed on the LDS write (row pad 2 floats makes the
-// transposed ds_write_b32 conflict-free), m/n-contiguous ones are written
-// with ds_write_b128.  Register-staged double buffering: the next tile's
-// global loads are issued before the current tile's MFMAs, written to the
-// other LDS buffer after them, one barrier per K-tile.
+//
+// Staging: every operand tile goes global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, one 1 KiB wave-instruction = 64 lanes x 16 B at
+// lane-linear LDS addresses, per-lane gathered source addresses; lanes whose
+// tap is out of bounds point at a 64 B zero page).  Two LDS images:
+//   KC  operand contiguous along k in memory (x for FWD, dy and W^T for
+//       DGRAD): image [rows][BK], 16 B quads XOR-swizzled by row
+//       (pq = q ^ f(row)), read with ds_read_b128 — conflict-free;
+//   MC  operand contiguous along m/n (W for FWD, x and dy for WGRAD):
+//       image [BK][cols], read with ds_read_b32, consecutive lanes
+//       consecutive columns — conflict-free.
+// MFMA k order: lane half h consumes k in [h*BK/2, (h+1)*BK/2), step s = k
+// offset, identical for both images.  Double-buffered LDS, one barrier per
+// K-tile: tile t+1's DMA is in flight while tile t's MFMAs run.
 // Split-K (grid.z) writes fp32 slabs reduced in a fixed order by a second
 // kernel, so results are bitwise reproducible (no float atomics).
+// c_in % 4 != 0 (conv1, c_in = 3) is handled by virtual channel padding:
+// k runs over (r, c, ci4 < 4); the input buffer must hold 4 readable
+// (finite; the engine keeps them zero) channels per pixel and the weight
+// rows ci4 >= c_in read as zeros.
 #include "jr_common.h"
+
+#include <array>
+#include <map>
+#include <mutex>
 
 namespace jr {
 
@@ -27,39 +45,114 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum { OP_FWD = 0, OP_DGRAD = 1, OP_WGRAD = 2 };
 
+// 64 B of zeros in global memory: the DMA source of out-of-bounds taps.
+__device__ __attribute__((aligned(64))) float g_zero_page[16];
+
 struct ConvArgs {
   const float* A;
   const float* B;
   float* C;
-  int M, N, K;
-  int n, h, w, cin, cout, kh, kw, sh, sw, ph, pw, ho, wo;
-  int xo, xs, yo, ys;     // channel slices of x and of dy/y
-  int c_off, c_stride;    // output addressing: C[m*c_stride + c_off + n]
+  int M, N, K;                // GEMM dims (DGRAD: of this phase)
+  int n, h, w, cin, cp, cout, kh, kw, sh, sw, ph, pw, ho, wo;
+  int xo, xs, yo, ys;         // channel slices of x and of dy
+  int c_off, c_stride;        // output addressing
   int accumulate;
-  int ktiles;             // total K tiles
-  int kt_per_split;
-  int ntn;                // number of N tiles
-  long long slab_elems;   // M*N (split-K slabs)
+  int ktiles, kt_per_split, ntn;
+  long long slab_elems;       // M*N (split-K slabs)
+  // DGRAD phase (py,px): taps r = r0 + sh*a (a < na), c = c0 + sw*b (b < nb);
+  // m = (b, u, v) over hc x wc; ih = sh*u + py; oh = u + ey - a.
+  int py, px, r0, c0, na, nb, ey, ex, hc, wc;
 };
 
-template <int OP, int BM, int BN, int WM, int WN, bool SCALAR>
-__global__ void __launch_bounds__(256) k_conv_f32(ConvArgs g) {
-  constexpr int BK = 16;
+// Output element offset of GEMM row m (column 0), or -1 to drop the row.
+template <int OP>
+__device__ __forceinline__ long long out_row(const ConvArgs& g, int m) {
+  if constexpr (OP == OP_FWD) {
+    return (long long)m * g.c_stride + g.c_off;
+  } else if constexpr (OP == OP_DGRAD) {
+    const int hw = g.hc * g.wc;
+    const int b = m / hw, rem = m - b * hw;
+    const int u = rem / g.wc, v = rem - u * g.wc;
+    const long long pix = ((long long)b * g.h + g.sh * u + g.py) * g.w + g.sw * v + g.px;
+    return pix * g.c_stride + g.c_off;
+  } else {
+    if (g.cp == g.cin) return (long long)m * g.N;
+    const int rc = m / g.cp, ci = m - rc * g.cp;
+    if (ci >= g.cin) return -1;
+    return ((long long)rc * g.cin + ci) * g.N;
+  }
+}
+
+// s_waitcnt vmcnt(n) + lgkmcnt(0) for a wave-uniform runtime n (immediate
+// operand: switch over the values a K-tile pipeline can need).
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// Advance the mixed-radix counter (z, y, x) (radices ly, lx) by BK along x.
+// multi (wave-uniform) = lx < BK: more than one carry is possible.
+template <int BK>
+__device__ __forceinline__ void adv_mixed_t(int& x, int& y, int& z, int lx, int ly, bool multi) {
+  x += BK;
+  if (!multi) {
+    const bool c1 = x >= lx;
+    x = c1 ? x - lx : x;
+    y += c1 ? 1 : 0;
+    const bool c2 = y == ly;
+    y = c2 ? 0 : y;
+    z += c2 ? 1 : 0;
+  } else {
+    while (x >= lx) {
+      x -= lx;
+      if (++y == ly) { y = 0; ++z; }
+    }
+  }
+}
+#define adv_mixed(x, y, z, lx, ly, multi) adv_mixed_t<BK>(x, y, z, lx, ly, multi)
+
+__device__ __forceinline__ void dma16(const float* src, float* lds_chunk) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_chunk, 16, 0, 0);
+}
+
+// DBG (diagnostic builds only, jr_conv2d_debug_time): 1 = no MFMA,
+// 2 = no DMA after the first tile (results are wrong in both).
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, int DBG = 0>
+__global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
+  constexpr int WGN = 4 / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int WGN = BN / WN;
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
-  constexpr bool A_TRANS = (OP != OP_WGRAD) && !SCALAR;  // k-contiguous A
-  constexpr bool B_TRANS = (OP == OP_DGRAD);             // k-contiguous B
-  constexpr int LDA = BM + (A_TRANS ? 2 : 0);
-  constexpr int LDB = BN + (B_TRANS ? 2 : 0);
-  constexpr int ASZ = BK * LDA, BSZ = BK * LDB;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (ASZ + BSZ)];
-  float* As0 = smem;
-  float* Bs0 = smem + 2 * ASZ;
+  static_assert(WM % 32 == 0 && WN % 32 == 0, "wave tile must be a multiple of 32x32");
+  constexpr int QPR = BK / 4;                 // 16 B quads per KC row
+  constexpr int RPI = 64 / QPR;               // KC rows per DMA instruction
+  constexpr int SWZ = 16 / QPR;               // rows sharing one swizzle value
+  constexpr int HALF = BK / 2;                // k per lane half
+  constexpr bool A_KC = (OP != OP_WGRAD);
+  constexpr bool B_KC = (OP == OP_DGRAD);
+  constexpr int ASZ = BM * BK, BSZ = BN * BK;  // floats per image
+  constexpr int A_INSTR = ASZ / 256, B_INSTR = BSZ / 256;
+  constexpr int A_PW = (A_INSTR + 3) / 4, B_PW = (B_INSTR + 3) / 4;  // per wave
+  static_assert(ASZ % 256 == 0 && BSZ % 256 == 0, "tile must be whole DMA instructions");
+  __shared__ __attribute__((aligned(1024))) float smem[NBUF * (ASZ + BSZ)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm0 = (wave / WGN) * WM;
   const int wn0 = (wave % WGN) * WN;
 
@@ -68,21 +161,24 @@ __global__ void __launch_bounds__(256) k_conv_f32(ConvArgs g) {
   const int m0 = mt * BM, n0 = nt * BN;
   const int kt0 = blockIdx.z * g.kt_per_split;
   const int kt1 = min(g.ktiles, kt0 + g.kt_per_split);
+  const float* zp = g_zero_page;
 
-  // ------------------------------------------------------------------ A state
-  // A_TRANS: BM/64 float4 per thread, (kq = idx&3, row = idx>>2)
-  // WGRAD vector: BM/64 float4 per thread, (m4 = idx % (BM/4), kk = idx / (BM/4))
-  // SCALAR: BM*BK/256 scalars per thread, (row = idx % BM, kk = idx / BM)
-  constexpr int NA = SCALAR ? (BM * BK / 256) : (BM / 64);
-  int a_p0[NA], a_p1[NA], a_base[NA];  // per-row precomputed geometry
-  int a_kk[NA];
+  // ---------------------------------------------------------------- A state
+  // KC: instr j covers rows j*RPI.. ; lane -> (row, logical quad q)
+  // MC: instr j covers floats [256j, 256j+256) of [BK][BM]: lane -> (krow, col)
+  int a_p0[A_PW], a_p1[A_PW], a_p2[A_PW];   // per-slot geometry fixed over K
+  int a_s0[A_PW], a_s1[A_PW], a_s2[A_PW];   // per-slot state advanced per K-tile
 #pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    const int idx = tid + i * 256;
-    if constexpr (SCALAR) {
-      const int row = idx % BM;
-      a_kk[i] = idx / BM;
+  for (int i = 0; i < A_PW; ++i) {
+    const int j = wave + 4 * i;
+    a_p0[i] = a_p1[i] = a_p2[i] = 0;
+    a_s0[i] = a_s1[i] = a_s2[i] = 0;
+    if (j >= A_INSTR) continue;
+    if constexpr (A_KC) {
+      const int row = j * RPI + lane / QPR;
+      const int q = (lane % QPR) ^ ((row / SWZ) % QPR);
       const int m = m0 + row;
+      const int k = kt0 * BK + q * 4;
       if constexpr (OP == OP_FWD) {
         if (m < g.M) {
           const int hw = g.ho * g.wo;
@@ -90,216 +186,142 @@ __global__ void __launch_bounds__(256) k_conv_f32(ConvArgs g) {
           const int oh = rem / g.wo, ow = rem - oh * g.wo;
           a_p0[i] = oh * g.sh - g.ph;
           a_p1[i] = ow * g.sw - g.pw;
-          a_base[i] = b * g.h * g.w;
+          a_p2[i] = b * g.h * g.w;
         } else {
-          a_p0[i] = -(1 << 28); a_p1[i] = 0; a_base[i] = 0;
+          a_p0[i] = -(1 << 28);
         }
-      } else {  // WGRAD scalar: m = (r,c,ci)
+        const int rc = k / g.cp;
+        a_s2[i] = k - rc * g.cp;          // ci
+        a_s0[i] = rc / g.kw;              // r
+        a_s1[i] = rc - a_s0[i] * g.kw;    // c
+      } else {  // DGRAD: m = (b,u,v) of the phase, k = (a, bb, co)
         if (m < g.M) {
-          const int rc = m / g.cin, ci = m - rc * g.cin;
-          const int r = rc / g.kw, c = rc - r * g.kw;
-          a_p0[i] = r - g.ph; a_p1[i] = c - g.pw; a_base[i] = ci;
+          const int hw = g.hc * g.wc;
+          const int b = m / hw, rem = m - b * hw;
+          const int u = rem / g.wc, v = rem - u * g.wc;
+          a_p0[i] = u + g.ey;
+          a_p1[i] = v + g.ex;
+          a_p2[i] = b * g.ho * g.wo;
         } else {
-          a_p0[i] = -(1 << 28); a_p1[i] = 0; a_base[i] = 0;
+          a_p0[i] = -(1 << 28);
         }
+        const int ab = k / g.cout;
+        a_s2[i] = k - ab * g.cout;        // co
+        a_s0[i] = ab / g.nb;              // a
+        a_s1[i] = ab - a_s0[i] * g.nb;    // bb
       }
-    } else if constexpr (A_TRANS) {
-      const int row = idx >> 2;
-      a_kk[i] = (idx & 3) * 4;
-      const int m = m0 + row;
+    } else {  // WGRAD MC: m = (r,c,ci) fixed per slot, k = pixel advances
+      const int flat = j * 256 + lane * 4;
+      const int krow = flat / BM, col = flat - krow * BM;
+      const int m = m0 + col;
       if (m < g.M) {
-        if constexpr (OP == OP_FWD) {
-          const int hw = g.ho * g.wo;
-          const int b = m / hw, rem = m - b * hw;
-          const int oh = rem / g.wo, ow = rem - oh * g.wo;
-          a_p0[i] = oh * g.sh - g.ph;
-          a_p1[i] = ow * g.sw - g.pw;
-          a_base[i] = b * g.h * g.w;
-        } else {  // DGRAD: m = input pixel
-          const int hw = g.h * g.w;
-          const int b = m / hw, rem = m - b * hw;
-          const int ih = rem / g.w, iw = rem - ih * g.w;
-          a_p0[i] = ih + g.ph;
-          a_p1[i] = iw + g.pw;
-          a_base[i] = b * g.ho * g.wo;
-        }
-      } else {
-        a_p0[i] = -(1 << 28); a_p1[i] = -(1 << 28); a_base[i] = 0;
-      }
-    } else {  // WGRAD vector: m4 fixed, kk fixed
-      const int m4 = idx % (BM / 4);
-      a_kk[i] = idx / (BM / 4);
-      const int m = m0 + m4 * 4;
-      if (m < g.M) {
-        const int rc = m / g.cin, ci = m - rc * g.cin;
+        const int rc = m / g.cp, ci = m - rc * g.cp;
         const int r = rc / g.kw, c = rc - r * g.kw;
-        a_p0[i] = r - g.ph; a_p1[i] = c - g.pw; a_base[i] = ci;
+        a_p0[i] = r - g.ph;
+        a_p1[i] = c - g.pw;
+        a_p2[i] = ci;
       } else {
-        a_p0[i] = -(1 << 28); a_p1[i] = 0; a_base[i] = 0;
+        a_p0[i] = -(1 << 28);
       }
+      const int pix = kt0 * BK + krow;
+      const int hw = g.ho * g.wo;
+      a_s0[i] = pix / hw;                       // b
+      const int rem = pix - a_s0[i] * hw;
+      a_s1[i] = rem / g.wo;                     // oh
+      a_s2[i] = rem - a_s1[i] * g.wo;           // ow
+    }
+  }
+  // ---------------------------------------------------------------- B state
+  int b_p0[B_PW], b_s0[B_PW], b_s1[B_PW], b_s2[B_PW];
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int j = wave + 4 * i;
+    b_p0[i] = b_s0[i] = b_s1[i] = b_s2[i] = 0;
+    if (j >= B_INSTR) continue;
+    if constexpr (B_KC) {  // DGRAD: rows = ci, k = (a, bb, co)
+      const int row = j * RPI + lane / QPR;
+      const int q = (lane % QPR) ^ ((row / SWZ) % QPR);
+      const int nn = n0 + row;
+      b_p0[i] = nn < g.N ? nn : -1;
+      const int k = kt0 * BK + q * 4;
+      const int ab = k / g.cout;
+      b_s2[i] = k - ab * g.cout;
+      b_s0[i] = ab / g.nb;
+      b_s1[i] = ab - b_s0[i] * g.nb;
+    } else {  // MC: rows = k, cols = n
+      const int flat = j * 256 + lane * 4;
+      const int krow = flat / BN, col = flat - krow * BN;
+      b_p0[i] = (n0 + col < g.N) ? n0 + col : -1;
+      b_s0[i] = kt0 * BK + krow;          // k
     }
   }
 
-  constexpr int NB_TOT = BK * BN / 4;            // float4 per B tile
-  constexpr int NB = (NB_TOT + 255) / 256;
-
-  float4 ra[SCALAR ? 1 : NA];
-  float rs[SCALAR ? NA : 1];
-  float4 rb[NB];
-
-  auto load_tiles = [&](int kt) {
-    const int k0 = kt * BK;
-    // ---------------- A
-    if constexpr (SCALAR) {
+  // Branch-free address generation: every operand slot keeps its k-position
+  // as a mixed-radix counter advanced by BK per tile (one conditional carry
+  // when the inner radix >= BK, the common case; a uniform slow path
+  // otherwise), and out-of-range taps select the zero page.
+  const bool a_multi = A_KC ? ((OP == OP_FWD ? g.cp : g.cout) < BK) : (g.wo < BK);
+  const bool b_multi = B_KC ? (g.cout < BK) : false;
+  auto issue = [&](int kt, float* __restrict__ As, float* __restrict__ Bs) {
+    (void)kt;
+    // -------------------------------------------------------------- A
 #pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int k = k0 + a_kk[i];
-        float v = 0.f;
+    for (int i = 0; i < A_PW; ++i) {
+      const int j = wave + 4 * i;
+      if (j >= A_INSTR) continue;
+      const float* src;
+      if constexpr (OP == OP_FWD) {
+        const int hi = a_p0[i] + a_s0[i], wi = a_p1[i] + a_s1[i];
+        const bool ok = (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w && a_s0[i] < g.kh;
+        const float* p = g.A + ((a_p2[i] + hi * g.w + wi) * g.xs + g.xo + a_s2[i]);
+        src = ok ? p : zp;
+        adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cp, g.kw, a_multi);
+      } else if constexpr (OP == OP_DGRAD) {
+        const int oh = a_p0[i] - a_s0[i], ow = a_p1[i] - a_s1[i];
+        const bool ok = (unsigned)oh < (unsigned)g.ho && (unsigned)ow < (unsigned)g.wo && a_s0[i] < g.na;
+        const float* p = g.A + ((a_p2[i] + oh * g.wo + ow) * g.ys + g.yo + a_s2[i]);
+        src = ok ? p : zp;
+        adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cout, g.nb, a_multi);
+      } else {  // WGRAD
+        const int hi = a_s1[i] * g.sh + a_p0[i], wi = a_s2[i] * g.sw + a_p1[i];
+        const bool ok = a_s0[i] < g.n && (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w;
+        const float* p = g.A + (((a_s0[i] * g.h + hi) * g.w + wi) * g.xs + g.xo + a_p2[i]);
+        src = ok ? p : zp;
+        adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.wo, g.ho, a_multi);
+      }
+      dma16(src, As + j * 256);
+    }
+    // -------------------------------------------------------------- B
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      const int j = wave + 4 * i;
+      if (j >= B_INSTR) continue;
+      const float* src;
+      if constexpr (B_KC) {  // DGRAD: W[(r0+sh*a, c0+sw*bb)][ci][co]
+        const bool ok = b_p0[i] >= 0 && b_s0[i] < g.na;
+        const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
+        const float* p = g.B + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
+        src = ok ? p : zp;
+        adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
+      } else {
+        const int k = b_s0[i];
+        bool ok = b_p0[i] >= 0 && k < g.K;
+        const float* p;
         if constexpr (OP == OP_FWD) {
-          if (k < g.K) {
-            const int rc = k / g.cin, ci = k - rc * g.cin;
-            const int r = rc / g.kw, c = rc - r * g.kw;
-            const int hi = a_p0[i] + r, wi = a_p1[i] + c;
-            if ((unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w)
-              v = g.A[(long long)(a_base[i] + hi * g.w + wi) * g.xs + g.xo + ci];
+          int row = k;
+          if (g.cp != g.cin) {  // virtual channel padding (c_in % 4 != 0): uniform branch
+            const int rc = k / g.cp, ci = k - rc * g.cp;
+            ok = ok && ci < g.cin;
+            row = rc * g.cin + ci;
           }
-        } else {  // WGRAD scalar
-          if (k < g.K) {
-            const int hw = g.ho * g.wo;
-            const int b = k / hw, rem = k - b * hw;
-            const int oh = rem / g.wo, ow = rem - oh * g.wo;
-            const int hi = oh * g.sh + a_p0[i], wi = ow * g.sw + a_p1[i];
-            if ((unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w)
-              v = g.A[(long long)((b * g.h + hi) * g.w + wi) * g.xs + g.xo + a_base[i]];
-          }
+          p = g.B + (row * g.N + b_p0[i]);
+        } else {  // WGRAD: dy rows
+          p = g.B + (k * g.ys + g.yo + b_p0[i]);
         }
-        rs[i] = v;
+        src = ok ? p : zp;
+        b_s0[i] += BK;
       }
-    } else if constexpr (A_TRANS) {
-      const int cred = (OP == OP_FWD) ? g.cin : g.cout;
-      const int rc = k0 / cred, ch0 = k0 - rc * cred;
-      const int r = rc / g.kw, c = rc - r * g.kw;
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (OP == OP_FWD) {
-          const int hi = a_p0[i] + r, wi = a_p1[i] + c;
-          if ((unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w)
-            v = *reinterpret_cast<const float4*>(
-                g.A + (long long)(a_base[i] + hi * g.w + wi) * g.xs + g.xo + ch0 + a_kk[i]);
-        } else {  // DGRAD
-          const int hn = a_p0[i] - r, wn = a_p1[i] - c;
-          bool ok;
-          int oh, ow;
-          if (g.sh == 1 && g.sw == 1) {
-            oh = hn; ow = wn;
-            ok = (unsigned)oh < (unsigned)g.ho && (unsigned)ow < (unsigned)g.wo;
-          } else {
-            ok = hn >= 0 && wn >= 0 && (hn % g.sh) == 0 && (wn % g.sw) == 0;
-            oh = hn / g.sh; ow = wn / g.sw;
-            ok = ok && oh < g.ho && ow < g.wo;
-          }
-          if (ok)
-            v = *reinterpret_cast<const float4*>(
-                g.A + (long long)(a_base[i] + oh * g.wo + ow) * g.ys + g.yo + ch0 + a_kk[i]);
-        }
-        ra[i] = v;
-      }
-    } else {  // WGRAD vector
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        const int k = k0 + a_kk[i];
-        if (k < g.K) {
-          const int hw = g.ho * g.wo;
-          const int b = k / hw, rem = k - b * hw;
-          const int oh = rem / g.wo, ow = rem - oh * g.wo;
-          const int hi = oh * g.sh + a_p0[i], wi = ow * g.sw + a_p1[i];
-          if ((unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w)
-            v = *reinterpret_cast<const float4*>(
-                g.A + (long long)((b * g.h + hi) * g.w + wi) * g.xs + g.xo + a_base[i]);
-        }
-        ra[i] = v;
-      }
-    }
-    // ---------------- B
-    if constexpr (B_TRANS) {  // DGRAD: B[k=(r,c,co)][n=ci] = W[(rc*cin + ci)*cout + co]
-      const int rc = k0 / g.cout, co0 = k0 - rc * g.cout;
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int idx = tid + i * 256;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (idx < NB_TOT) {
-          const int kq = idx & 3, col = idx >> 2;
-          const int nn = n0 + col;
-          if (nn < g.N)
-            v = *reinterpret_cast<const float4*>(g.B + ((long long)rc * g.cin + nn) * g.cout + co0 + kq * 4);
-        }
-        rb[i] = v;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int idx = tid + i * 256;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (idx < NB_TOT) {
-          const int n4 = idx % (BN / 4), kk = idx / (BN / 4);
-          const int k = k0 + kk, nn = n0 + n4 * 4;
-          if (k < g.K && nn < g.N) {
-            if constexpr (OP == OP_FWD)
-              v = *reinterpret_cast<const float4*>(g.B + (long long)k * g.N + nn);
-            else  // WGRAD: dy rows
-              v = *reinterpret_cast<const float4*>(g.B + (long long)k * g.ys + g.yo + nn);
-          }
-        }
-        rb[i] = v;
-      }
-    }
-  };
-
-  auto store_tiles = [&](int buf) {
-    float* As = As0 + buf * ASZ;
-    float* Bs = Bs0 + buf * BSZ;
-    if constexpr (SCALAR) {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int idx = tid + i * 256;
-        As[a_kk[i] * LDA + (idx % BM)] = rs[i];
-      }
-    } else if constexpr (A_TRANS) {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int row = (tid + i * 256) >> 2;
-        float* p = As + a_kk[i] * LDA + row;
-        p[0] = ra[i].x; p[LDA] = ra[i].y; p[2 * LDA] = ra[i].z; p[3 * LDA] = ra[i].w;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int idx = tid + i * 256;
-        const int m4 = idx % (BM / 4);
-        *reinterpret_cast<float4*>(As + a_kk[i] * LDA + m4 * 4) = ra[i];
-      }
-    }
-    if constexpr (B_TRANS) {
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int idx = tid + i * 256;
-        if (idx < NB_TOT) {
-          const int kq = idx & 3, col = idx >> 2;
-          float* p = Bs + kq * 4 * LDB + col;
-          p[0] = rb[i].x; p[LDB] = rb[i].y; p[2 * LDB] = rb[i].z; p[3 * LDB] = rb[i].w;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int idx = tid + i * 256;
-        if (idx < NB_TOT) {
-          const int n4 = idx % (BN / 4), kk = idx / (BN / 4);
-          *reinterpret_cast<float4*>(Bs + kk * LDB + n4 * 4) = rb[i];
-        }
-      }
+      dma16(src, Bs + j * 256);
     }
   };
 
@@ -311,242 +333,453 @@ __global__ void __launch_bounds__(256) k_conv_f32(ConvArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  const int l31 = lane & 31, lh = lane >> 5;
+  // DMA wave-instructions this wave issues per K-tile (wave-uniform; a
+  // compile-time constant when every wave issues the same number)
+  constexpr bool UNIFORM_DMA = (A_INSTR % 4 == 0) && (B_INSTR % 4 == 0);
+  int per_tile = A_INSTR / 4 + B_INSTR / 4;
+  if constexpr (!UNIFORM_DMA) {
+    per_tile = 0;
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) per_tile += (wave + 4 * i < A_INSTR);
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) per_tile += (wave + 4 * i < B_INSTR);
+  }
+
   if (kt0 < kt1) {
-    load_tiles(kt0);
-    store_tiles(0);
-    __syncthreads();
-    const int l31 = lane & 31, lhi = lane >> 5;
+    // prologue: tiles kt0 .. kt0+NBUF-2 in flight
+#pragma unroll
+    for (int p = 0; p < NBUF - 1; ++p)
+      if (kt0 + p < kt1) issue(kt0 + p, smem + p * (ASZ + BSZ), smem + p * (ASZ + BSZ) + ASZ);
+    wait_vmcnt(per_tile * min(NBUF - 2, kt1 - kt0 - 1));
+    __builtin_amdgcn_s_barrier();
+    int cur = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
-      const int cur = (kt - kt0) & 1;
-      const bool more = kt + 1 < kt1;
-      if (more) load_tiles(kt + 1);
-      const float* As = As0 + cur * ASZ;
-      const float* Bs = Bs0 + cur * BSZ;
+      const int nxt = cur == 0 ? NBUF - 1 : cur - 1;
+      float af[TM][HALF], bfr[TN][HALF];
+      // Reads of tile kt and the DMA of tile kt+NBUF-1 through __restrict__
+      // views of two different buffers: the noalias scopes let hipcc's
+      // waitcnt pass see that the ds_reads need not wait for the LDS-DMA
+      // still in flight (without them it drains every DMA first).
+      auto stage = [&](const float* __restrict__ As, const float* __restrict__ Bs, float* __restrict__ wA,
+                       float* __restrict__ wB) {
+      // 1) all of this lane's operand fragments of tile kt: LDS -> VGPRs,
+      //    before this iteration's DMA is issued.
 #pragma unroll
-      for (int ks = 0; ks < BK / 2; ++ks) {
-        const int k = ks * 2 + lhi;
-        float a[TM], b[TN];
+      for (int i = 0; i < TM; ++i) {
+        if constexpr (A_KC) {
+          const int row = wm0 + i * 32 + l31;
+          const int f = (row / SWZ) % QPR;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = As[k * LDA + wm0 + i * 32 + l31];
+          for (int t = 0; t < QPR / 2; ++t) {
+            const float4 v = *reinterpret_cast<const float4*>(As + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
+            af[i][4 * t + 0] = v.x; af[i][4 * t + 1] = v.y; af[i][4 * t + 2] = v.z; af[i][4 * t + 3] = v.w;
+          }
+        } else {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = Bs[k * LDB + wn0 + j * 32 + l31];
+          for (int s = 0; s < HALF; ++s) af[i][s] = As[(lh * HALF + s) * BM + wm0 + i * 32 + l31];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (B_KC) {
+          const int row = wn0 + j * 32 + l31;
+          const int f = (row / SWZ) % QPR;
+#pragma unroll
+          for (int t = 0; t < QPR / 2; ++t) {
+            const float4 v = *reinterpret_cast<const float4*>(Bs + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
+            bfr[j][4 * t + 0] = v.x; bfr[j][4 * t + 1] = v.y; bfr[j][4 * t + 2] = v.z; bfr[j][4 * t + 3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < HALF; ++s) bfr[j][s] = Bs[(lh * HALF + s) * BN + wn0 + j * 32 + l31];
+        }
+      }
+      // 2) DMA of tile kt+NBUF-1 into the buffer read in iteration kt-1
+      //    (released by the barrier that ended it)
+      if (DBG != 2 && kt + NBUF - 1 < kt1) issue(kt + NBUF - 1, wA, wB);
+      };
+      stage(smem + cur * (ASZ + BSZ), smem + cur * (ASZ + BSZ) + ASZ, smem + nxt * (ASZ + BSZ),
+            smem + nxt * (ASZ + BSZ) + ASZ);
+      // 3) MFMAs from registers while NBUF-1 tiles of DMA are in flight
+#pragma unroll
+      for (int s = 0; s < HALF; ++s)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-      }
-      if (more) store_tiles(cur ^ 1);
-      __syncthreads();
+            if constexpr (DBG == 1) acc[i][j][s & 15] += af[i][s] * bfr[j][s];
+            else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+      // 4) tile kt+1 landed (this wave's newer DMAs may stay in flight), then
+      //    one barrier: every wave's part of tile kt+1 is in LDS and every
+      //    wave is done reading tile kt.  sched_barrier keeps hipcc from
+      //    sinking the register-only MFMAs below the wait.
+      __builtin_amdgcn_sched_barrier(0);
+      wait_vmcnt(per_tile * max(0, min(NBUF - 2, kt1 - kt - 2)));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      cur = cur + 1 == NBUF ? 0 : cur + 1;
     }
   }
 
   // ---------------------------------------------------------------- epilogue
   const bool split = gridDim.z > 1;
-  float* C = g.C;
-  long long cs = g.c_stride, co = g.c_off;
-  if (split) {
-    C = g.C + (long long)blockIdx.z * g.slab_elems;
-    cs = g.N; co = 0;
-  }
-  const int col = lane & 31;
-  const int rbase = 4 * (lane >> 5);
+  float* C = split ? g.C + (long long)blockIdx.z * g.slab_elems : g.C;
+  const int rbase = 4 * lh;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn0 + j * 32 + col;
-      if (n >= g.N) continue;
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+      if (m >= g.M) continue;
+      const long long base = split ? (long long)m * g.N : out_row<OP>(g, m);
+      if (base < 0) continue;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
-        if (m < g.M) {
-          float* p = C + (long long)m * cs + co + n;
-          if (!split && g.accumulate) *p += acc[i][j][r];
-          else *p = acc[i][j][r];
-        }
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l31;
+        if (n >= g.N) continue;
+        float* p = C + base + n;
+        if (!split && g.accumulate) *p += acc[i][j][r];
+        else *p = acc[i][j][r];
       }
     }
   }
 }
 
-// out[m*c_stride + c_off + n] (+)= sum_z slab[z][m][n]   (fixed order)
-__global__ void k_splitk_reduce(const float* __restrict__ slab, int splits, long long slab_elems, int M,
-                                int N, float* out, int c_off, int c_stride, int accumulate) {
-  const long long total = (long long)M * N;
+// out[out_row(m) + n] (+)= sum_z slab[z][m][n]   (fixed order)
+template <int OP>
+__global__ void k_splitk_reduce(const float* __restrict__ slab, int splits, ConvArgs g, float* out) {
+  const long long total = (long long)g.M * g.N;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(e / g.N), n = (int)(e - (long long)m * g.N);
+    const long long base = out_row<OP>(g, m);
+    if (base < 0) continue;
     float s = slab[e];
-    for (int z = 1; z < splits; ++z) s += slab[z * slab_elems + e];
-    const long long m = e / N, n = e - m * N;
-    float* p = out + m * c_stride + c_off + n;
-    if (accumulate) s += *p;
+    for (int z = 1; z < splits; ++z) s += slab[z * g.slab_elems + e];
+    float* p = out + base + n;
+    if (g.accumulate) s += *p;
     *p = s;
   }
 }
 
 // ---------------------------------------------------------------- host side
 struct TileCfg {
-  int bm, bn;
+  int bm, bn, wgm, bk, nbuf;
+  double eff;  // relative MFMA efficiency guess used to rank padded work
 };
 
-static const TileCfg kCfgs[] = {{128, 128}, {128, 64}, {64, 64}, {128, 32}};
+// Candidate tiles (block BMxBN, WGM waves along M, K-tile BK).  The planner
+// ranks them by padded work / eff; jr_conv2d_autotune times them instead.
+// Keep in sync with launch_op's switch.
+static constexpr TileCfg kCfgs[] = {
+    {128, 128, 2, 16, 3, 1.00},  // 0: wave 64x64, 48 KiB LDS
+    {128, 128, 2, 32, 2, 1.00},  // 1: 64 KiB
+    {256, 64, 4, 16, 3, 1.00},   // 2: wave 64x64, 60 KiB
+    {128, 64, 2, 16, 4, 0.92},   // 3: wave 64x32, 48 KiB
+    {128, 64, 2, 32, 2, 0.92},   // 4: 48 KiB
+    {128, 96, 4, 16, 3, 0.90},   // 5: wave 32x96, 42 KiB
+    {256, 32, 4, 16, 4, 0.85},   // 6: wave 64x32, 72 KiB
+    {64, 64, 2, 32, 3, 0.75},    // 7: wave 32x32, 48 KiB
+    {128, 32, 4, 32, 3, 0.75},   // 8: wave 32x32, 60 KiB
+    {64, 128, 2, 32, 2, 0.80},   // 9: wave 32x64, 48 KiB
+    {128, 64, 2, 16, 2, 0.90},   // 10: wave 64x32, 24 KiB
+};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+struct Phase {
+  int py, px, r0, c0, na, nb, ey, ex, hc, wc;
+};
 
 struct Plan {
-  int cfg;      // index into kCfgs
-  int mt, nt;   // tiles
-  int ktiles;
-  int splits;
-  int kt_per_split;
-  bool scalar;
+  int cfg;
+  int M, N, K;
+  int mt, nt, ktiles, splits, kt_per_split;
 };
 
-static void gemm_dims(const jr_conv_desc* d, int op, int* M, int* N, int* K) {
-  const int P = d->n * d->ho * d->wo;
-  if (op == OP_FWD) { *M = P; *N = d->c_out; *K = d->kh * d->kw * d->c_in; }
-  else if (op == OP_DGRAD) { *M = d->n * d->h * d->w; *N = d->c_in; *K = d->kh * d->kw * d->c_out; }
-  else { *M = d->kh * d->kw * d->c_in; *N = d->c_out; *K = P; }
+static int chan_pad(int c) { return (c + 3) / 4 * 4; }
+
+static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
+  int k = 0;
+  for (int py = 0; py < d->stride_h; ++py) {
+    for (int px = 0; px < d->stride_w; ++px) {
+      Phase p{};
+      p.py = py; p.px = px;
+      p.hc = py < d->h ? (d->h - py + d->stride_h - 1) / d->stride_h : 0;
+      p.wc = px < d->w ? (d->w - px + d->stride_w - 1) / d->stride_w : 0;
+      p.r0 = (py + d->pad_h) % d->stride_h;
+      p.c0 = (px + d->pad_w) % d->stride_w;
+      p.na = p.r0 < d->kh ? (d->kh - p.r0 + d->stride_h - 1) / d->stride_h : 0;
+      p.nb = p.c0 < d->kw ? (d->kw - p.c0 + d->stride_w - 1) / d->stride_w : 0;
+      p.ey = (py + d->pad_h - p.r0) / d->stride_h;
+      p.ex = (px + d->pad_w - p.c0) / d->stride_w;
+      ph[k++] = p;
+    }
+  }
+  *nph = k;
 }
 
-static Plan make_plan(const jr_conv_desc* d, int op) {
-  int M, N, K;
-  gemm_dims(d, op, &M, &N, &K);
+static Plan plan_with(int cfg, int M, int N, int K) {
   Plan p{};
-  p.scalar = (op == OP_FWD && (d->c_in % 16) != 0) || (op == OP_WGRAD && (d->c_in % 4) != 0);
-  const double eff[] = {1.0, 0.92, 0.78, 0.78};
-  double best = 1e300;
-  for (int c = 0; c < 4; ++c) {
-    if (p.scalar && op == OP_FWD && c != 3 && c != 1) continue;  // scalar fwd: BM=128 only
-    const int bm = kCfgs[c].bm, bn = kCfgs[c].bn;
-    const double work = (double)ceil_div(M, bm) * bm * (double)ceil_div(N, bn) * bn / eff[c];
-    if (work < best * 0.999) { best = work; p.cfg = c; }
-  }
-  const int bm = kCfgs[p.cfg].bm, bn = kCfgs[p.cfg].bn;
-  p.mt = (int)ceil_div(M, bm);
-  p.nt = (int)ceil_div(N, bn);
-  p.ktiles = (int)ceil_div(K, 16);
-  // split-K: fill >= ~2 waves of blocks over 256 CUs, keep >= 8 K-tiles per split
+  p.M = M; p.N = N; p.K = K; p.cfg = cfg;
+  const TileCfg& t = kCfgs[cfg];
+  p.mt = (int)ceil_div(M, t.bm);
+  p.nt = (int)ceil_div(N, t.bn);
+  p.ktiles = (int)ceil_div(K, t.bk);
   const int tiles = p.mt * p.nt;
   int splits = 1;
-  const int target = 512;
+  const int target = 640;   // >= 2.5 blocks per CU
   if (tiles < target) {
     splits = (int)ceil_div(target, tiles);
-    const int max_by_k = p.ktiles / 8 > 0 ? p.ktiles / 8 : 1;
-    if (splits > max_by_k) splits = max_by_k;
-    if (splits > 256) splits = 256;
-    if (splits < 1) splits = 1;
+    const int max_by_k = std::max(1, p.ktiles / 8);
+    splits = std::min(std::min(splits, max_by_k), 256);
   }
-  p.kt_per_split = (int)ceil_div(p.ktiles, splits);
-  p.splits = (int)ceil_div(p.ktiles, p.kt_per_split);
+  p.kt_per_split = (int)ceil_div(std::max(p.ktiles, 1), splits);
+  p.splits = (int)ceil_div(std::max(p.ktiles, 1), p.kt_per_split);
   return p;
 }
 
-static size_t plan_ws_bytes(const jr_conv_desc* d, int op) {
-  const Plan p = make_plan(d, op);
-  if (p.splits <= 1) return 0;
-  int M, N, K;
-  gemm_dims(d, op, &M, &N, &K);
-  return (size_t)p.splits * (size_t)M * (size_t)N * sizeof(float);
+static int heuristic_cfg(int M, int N, int K) {
+  double best = 1e300;
+  int bc = 0;
+  for (int c = 0; c < kNumCfgs; ++c) {
+    const TileCfg& t = kCfgs[c];
+    const double tiles = (double)ceil_div(M, t.bm) * ceil_div(N, t.bn);
+    double work = tiles * t.bm * t.bn / t.eff;
+    // grids that cannot fill the 256 CUs and cannot be split along K lose
+    if (tiles < 256 && ceil_div(K, t.bk) < 32) work *= 256.0 / tiles;
+    if (work < best * 0.999) { best = work; bc = c; }
+  }
+  return bc;
 }
 
-template <int OP, int BM, int BN, int WM, int WN, bool SC>
+// Autotune cache: (op, GEMM dims, conv geometry) -> best config.
+typedef std::array<int, 12> TuneKey;
+static std::mutex g_tune_mu;
+static std::map<TuneKey, int> g_tuned;
+
+static TuneKey tune_key(int op, int M, int N, int K, const jr_conv_desc* d) {
+  return TuneKey{op, M, N, K, d->h, d->w, d->kh, d->kw, d->stride_h, d->c_in, d->c_out, d->n};
+}
+
+static Plan make_plan(int op, int M, int N, int K, const jr_conv_desc* d, int force_cfg = -1) {
+  int cfg = force_cfg;
+  if (cfg < 0) {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    auto it = g_tuned.find(tune_key(op, M, N, K, d));
+    if (it != g_tuned.end()) cfg = it->second;
+  }
+  if (cfg < 0) cfg = heuristic_cfg(M, N, K);
+  return plan_with(cfg, M, N, K);
+}
+
+static size_t plan_ws(const Plan& p) {
+  return p.splits > 1 ? (size_t)p.splits * (size_t)p.M * (size_t)p.N * sizeof(float) : 0;
+}
+
+template <int OP, int C>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((k_conv_f32<OP, BM, BN, WM, WN, SC>), grid, dim3(256), 0, s, a);
+  constexpr TileCfg t = kCfgs[C];
+  hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf>), grid, dim3(256), 0, s, a);
 }
 
-template <int OP, bool SC>
+template <int OP>
 static void launch_op(int cfg, const ConvArgs& a, dim3 grid, hipStream_t s) {
   switch (cfg) {
-    case 0: launch_cfg<OP, 128, 128, 64, 64, SC>(a, grid, s); break;
-    case 1: launch_cfg<OP, 128, 64, 64, 32, SC>(a, grid, s); break;
-    case 2: launch_cfg<OP, 64, 64, 32, 32, SC>(a, grid, s); break;
-    default: launch_cfg<OP, 128, 32, 32, 32, SC>(a, grid, s); break;
+    case 0: launch_cfg<OP, 0>(a, grid, s); break;
+    case 1: launch_cfg<OP, 1>(a, grid, s); break;
+    case 2: launch_cfg<OP, 2>(a, grid, s); break;
+    case 3: launch_cfg<OP, 3>(a, grid, s); break;
+    case 4: launch_cfg<OP, 4>(a, grid, s); break;
+    case 5: launch_cfg<OP, 5>(a, grid, s); break;
+    case 6: launch_cfg<OP, 6>(a, grid, s); break;
+    case 7: launch_cfg<OP, 7>(a, grid, s); break;
+    case 8: launch_cfg<OP, 8>(a, grid, s); break;
+    case 9: launch_cfg<OP, 9>(a, grid, s); break;
+    default: launch_cfg<OP, 10>(a, grid, s); break;
   }
 }
 
-static int validate(const jr_conv_desc* d) {
+static int validate(const jr_conv_desc* d, int op) {
   if (!d) return fail(JR_ERR_INVALID, "conv: null descriptor");
+  if (op < OP_FWD || op > OP_WGRAD) return fail(JR_ERR_INVALID, "conv: bad op");
   if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c_in <= 0 || d->c_out <= 0 || d->kh <= 0 ||
       d->kw <= 0 || d->stride_h <= 0 || d->stride_w <= 0 || d->pad_h < 0 || d->pad_w < 0)
     return fail(JR_ERR_INVALID, "conv: non-positive dimension");
   const int ho = (d->h + 2 * d->pad_h - d->kh) / d->stride_h + 1;
   const int wo = (d->w + 2 * d->pad_w - d->kw) / d->stride_w + 1;
-  if (ho != d->ho || wo != d->wo)
+  if (ho != d->ho || wo != d->wo || ho <= 0 || wo <= 0)
     return fail(JR_ERR_INVALID, "conv: ho/wo inconsistent with h,w,k,stride,pad");
-  if (d->x_c_off < 0 || d->x_c_off + d->c_in > d->x_c_stride)
-    return fail(JR_ERR_INVALID, "conv: input channel slice out of range");
+  if (d->pad_h >= d->kh || d->pad_w >= d->kw)
+    return fail(JR_ERR_INVALID, "conv: padding must be smaller than the kernel");
+  const int cp = chan_pad(d->c_in);
+  if (d->x_c_off < 0 || d->x_c_off + cp > d->x_c_stride)
+    return fail(JR_ERR_INVALID, "conv: input channel slice (padded to a multiple of 4) out of range");
   if (d->y_c_off < 0 || d->y_c_off + d->c_out > d->y_c_stride)
     return fail(JR_ERR_INVALID, "conv: output channel slice out of range");
-  if (d->c_out % 4 != 0 || d->y_c_stride % 4 != 0 || d->y_c_off % 4 != 0)
-    return fail(JR_ERR_INVALID, "conv: c_out, output stride and output offset must be multiples of 4");
-  if (d->c_in % 4 == 0 && (d->x_c_off % 4 != 0 || d->x_c_stride % 4 != 0))
-    return fail(JR_ERR_INVALID, "conv: input offset/stride must be multiples of 4 when c_in is");
-  const long long big = (long long)d->n * d->h * d->w * d->x_c_stride;
-  const long long bigo = (long long)d->n * d->ho * d->wo * d->y_c_stride;
-  if (big >= (1LL << 31) * 4 || bigo >= (1LL << 31) * 4)
-    return fail(JR_ERR_INVALID, "conv: tensor too large for 32-bit pixel indexing");
+  if (d->c_out % 16 != 0)
+    return fail(JR_ERR_UNSUPPORTED, "conv: c_out must be a multiple of 16");
+  if (d->x_c_off % 4 || d->x_c_stride % 4 || d->y_c_off % 4 || d->y_c_stride % 4)
+    return fail(JR_ERR_INVALID, "conv: channel offsets and strides must be multiples of 4");
+  if (op == OP_DGRAD && d->c_in % 4 != 0)
+    return fail(JR_ERR_UNSUPPORTED, "conv bwd_data: c_in must be a multiple of 4");
+  if (d->stride_h * d->stride_w > 64) return fail(JR_ERR_UNSUPPORTED, "conv: stride too large");
+  const long long xin = (long long)d->n * d->h * d->w * d->x_c_stride;
+  const long long yout = (long long)d->n * d->ho * d->wo * d->y_c_stride;
+  const long long wsz = (long long)d->kh * d->kw * d->c_in * d->c_out;
+  if (xin >= (1LL << 31) || yout >= (1LL << 31) || wsz >= (1LL << 31))
+    return fail(JR_ERR_INVALID, "conv: tensor too large for 32-bit element offsets");
   return JR_OK;
 }
 
-static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, const void* B, void* C,
-                    int accumulate, void* ws, size_t ws_bytes, void* stream) {
-  int rc = validate(d);
-  if (rc) return rc;
-  if (dtype != JR_F32) return fail(JR_ERR_UNSUPPORTED, "conv: bf16 path not built in this round");
-  if (op == OP_DGRAD && d->c_out % 16 != 0)
-    return fail(JR_ERR_UNSUPPORTED, "conv bwd_data: c_out must be a multiple of 16");
-  if (op == OP_DGRAD && d->c_in % 4 != 0)
-    return fail(JR_ERR_UNSUPPORTED, "conv bwd_data: c_in must be a multiple of 4");
-  if (!A || !B || !C) return fail(JR_ERR_INVALID, "conv: null tensor pointer");
-  const Plan p = make_plan(d, op);
-  ConvArgs a{};
-  a.A = static_cast<const float*>(A);
-  a.B = static_cast<const float*>(B);
-  int M, N, K;
-  gemm_dims(d, op, &M, &N, &K);
-  a.M = M; a.N = N; a.K = K;
-  a.n = d->n; a.h = d->h; a.w = d->w; a.cin = d->c_in; a.cout = d->c_out;
+static void fill_common(ConvArgs& a, const jr_conv_desc* d) {
+  a.n = d->n; a.h = d->h; a.w = d->w; a.cin = d->c_in; a.cp = chan_pad(d->c_in); a.cout = d->c_out;
   a.kh = d->kh; a.kw = d->kw; a.sh = d->stride_h; a.sw = d->stride_w;
   a.ph = d->pad_h; a.pw = d->pad_w; a.ho = d->ho; a.wo = d->wo;
   a.xo = d->x_c_off; a.xs = d->x_c_stride; a.yo = d->y_c_off; a.ys = d->y_c_stride;
-  a.accumulate = accumulate;
+}
+
+// One GEMM (plus its split-K reduce) on the stream.
+template <int OP>
+static int run_gemm(ConvArgs a, const Plan& p, float* out, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (p.M <= 0 || p.N <= 0) return JR_OK;
+  a.M = p.M; a.N = p.N; a.K = p.K;
   a.ktiles = p.ktiles;
   a.kt_per_split = p.kt_per_split;
   a.ntn = p.nt;
-  a.slab_elems = (long long)M * N;
-  float* out = static_cast<float*>(C);
-  int c_off, c_stride;
-  if (op == OP_FWD) { c_off = d->y_c_off; c_stride = d->y_c_stride; }
-  else if (op == OP_DGRAD) { c_off = d->x_c_off; c_stride = d->x_c_stride; }
-  else { c_off = 0; c_stride = N; }
-  a.c_off = c_off; a.c_stride = c_stride;
+  a.slab_elems = (long long)p.M * p.N;
   if (p.splits > 1) {
-    const size_t need = (size_t)p.splits * (size_t)M * N * sizeof(float);
-    if (!ws || ws_bytes < need) return fail(JR_ERR_WORKSPACE, "conv: workspace too small for split-K");
+    if (!ws || ws_bytes < plan_ws(p)) return fail(JR_ERR_WORKSPACE, "conv: workspace too small for split-K");
     a.C = static_cast<float*>(ws);
   } else {
     a.C = out;
   }
-  hipStream_t s = as_stream(stream);
   dim3 grid(p.mt * p.nt, 1, p.splits);
-  if (op == OP_FWD) {
-    if (p.scalar) launch_op<OP_FWD, true>(p.cfg, a, grid, s);
-    else launch_op<OP_FWD, false>(p.cfg, a, grid, s);
-  } else if (op == OP_DGRAD) {
-    launch_op<OP_DGRAD, false>(p.cfg, a, grid, s);
-  } else {
-    if (p.scalar) launch_op<OP_WGRAD, true>(p.cfg, a, grid, s);
-    else launch_op<OP_WGRAD, false>(p.cfg, a, grid, s);
+  launch_op<OP>(p.cfg, a, grid, s);
+  int rc = check_launch("conv gemm");
+  if (rc || p.splits <= 1) return rc;
+  const long long total = (long long)p.M * p.N;
+  const int blocks = (int)std::min<long long>(ceil_div(total, 256), 4096);
+  hipLaunchKernelGGL((k_splitk_reduce<OP>), dim3(blocks), dim3(256), 0, s, (const float*)ws, p.splits, a, out);
+  return check_launch("conv split-k reduce");
+}
+
+static void gemm_dims(const jr_conv_desc* d, int op, const Phase* ph, int* M, int* N, int* K) {
+  const int cp = chan_pad(d->c_in);
+  if (op == OP_FWD) { *M = d->n * d->ho * d->wo; *N = d->c_out; *K = d->kh * d->kw * cp; }
+  else if (op == OP_WGRAD) { *M = d->kh * d->kw * cp; *N = d->c_out; *K = d->n * d->ho * d->wo; }
+  else { *M = d->n * ph->hc * ph->wc; *N = d->c_in; *K = ph->na * ph->nb * d->c_out; }
+}
+
+static Plan plan_for(const jr_conv_desc* d, int op, const Phase* ph, int force_cfg = -1) {
+  int M, N, K;
+  gemm_dims(d, op, ph, &M, &N, &K);
+  return make_plan(op, M, N, K, d, force_cfg);
+}
+
+// Workspace: the max over every candidate config, so any tuned choice fits.
+static size_t ws_bytes_for(const jr_conv_desc* d, int op) {
+  Phase ph[64];
+  int nph = 1;
+  if (op == OP_DGRAD) dgrad_phases(d, ph, &nph);
+  size_t w = 0;
+  for (int i = 0; i < nph; ++i) {
+    if (op == OP_DGRAD && (ph[i].na == 0 || ph[i].nb == 0 || ph[i].hc == 0 || ph[i].wc == 0)) continue;
+    for (int c = 0; c < kNumCfgs; ++c)
+      w = std::max(w, plan_ws(plan_for(d, op, op == OP_DGRAD ? &ph[i] : nullptr, c)));
   }
-  rc = check_launch("conv gemm");
+  return w;
+}
+
+// Runs the op; force_cfg >= 0 overrides the plan (autotuning).
+static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, const void* B, void* C,
+                    int accumulate, void* ws, size_t ws_bytes, void* stream, int force_cfg = -1,
+                    int only_phase = -1) {
+  int rc = validate(d, op);
   if (rc) return rc;
-  if (p.splits > 1) {
-    const long long total = (long long)M * N;
-    const int blocks = (int)std::min<long long>(ceil_div(total, 256), 4096);
-    hipLaunchKernelGGL(k_splitk_reduce, dim3(blocks), dim3(256), 0, s, (const float*)ws, p.splits,
-                       (long long)M * N, M, N, out, c_off, c_stride, accumulate);
-    rc = check_launch("conv split-k reduce");
+  if (dtype != JR_F32) return fail(JR_ERR_UNSUPPORTED, "conv: bf16 path not built in this round");
+  if (!A || !B || !C) return fail(JR_ERR_INVALID, "conv: null tensor pointer");
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15)
+    return fail(JR_ERR_INVALID, "conv: tensors must be 16-byte aligned");
+  ConvArgs a{};
+  fill_common(a, d);
+  a.A = static_cast<const float*>(A);
+  a.B = static_cast<const float*>(B);
+  a.accumulate = accumulate;
+  hipStream_t s = as_stream(stream);
+  float* out = static_cast<float*>(C);
+  if (op == OP_FWD) {
+    a.c_off = d->y_c_off; a.c_stride = d->y_c_stride;
+    return run_gemm<OP_FWD>(a, plan_for(d, op, nullptr, force_cfg), out, ws, ws_bytes, s);
   }
+  if (op == OP_WGRAD) {
+    a.c_off = 0; a.c_stride = d->c_out;
+    return run_gemm<OP_WGRAD>(a, plan_for(d, op, nullptr, force_cfg), out, ws, ws_bytes, s);
+  }
+  Phase ph[64];
+  int nph = 0;
+  dgrad_phases(d, ph, &nph);
+  a.c_off = d->x_c_off; a.c_stride = d->x_c_stride;
+  for (int i = 0; i < nph; ++i) {
+    if (only_phase >= 0 && i != only_phase) continue;
+    const Phase& p = ph[i];
+    if (p.hc == 0 || p.wc == 0) continue;
+    a.py = p.py; a.px = p.px; a.r0 = p.r0; a.c0 = p.c0; a.na = p.na; a.nb = p.nb;
+    a.ey = p.ey; a.ex = p.ex; a.hc = p.hc; a.wc = p.wc;
+    Plan pl;
+    if (p.na == 0 || p.nb == 0) {
+      // no tap reaches this phase: a K = 0 GEMM stores zeros (or leaves dx)
+      if (accumulate) continue;
+      pl = plan_with(heuristic_cfg(d->n * p.hc * p.wc, d->c_in, 16), d->n * p.hc * p.wc, d->c_in, 16);
+      pl.K = 0; pl.ktiles = 0; pl.splits = 1; pl.kt_per_split = 1;
+    } else {
+      pl = plan_for(d, op, &p, force_cfg);
+    }
+    rc = run_gemm<OP_DGRAD>(a, pl, out, ws, ws_bytes, s);
+    if (rc) return rc;
+  }
+  return JR_OK;
+}
+
+// Time every candidate config of each GEMM of this op (DGRAD: per phase) on
+// the caller's buffers (outputs are overwritten) and remember the fastest.
+static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, const void* B, void* C, void* ws,
+                    size_t ws_bytes, void* stream, int reps) {
+  int rc = validate(d, op);
+  if (rc) return rc;
+  Phase ph[64];
+  int nph = 1;
+  if (op == OP_DGRAD) dgrad_phases(d, ph, &nph);
+  hipStream_t s = as_stream(stream);
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+    return fail(JR_ERR_HIP, "autotune: hipEventCreate failed");
+  for (int i = 0; i < nph; ++i) {
+    if (op == OP_DGRAD && (ph[i].na == 0 || ph[i].nb == 0 || ph[i].hc == 0 || ph[i].wc == 0)) continue;
+    int M, N, K;
+    gemm_dims(d, op, op == OP_DGRAD ? &ph[i] : nullptr, &M, &N, &K);
+    float best_t = 1e30f;
+    int best_c = heuristic_cfg(M, N, K);
+    for (int c = 0; c < kNumCfgs; ++c) {
+      if (plan_ws(plan_with(c, M, N, K)) > ws_bytes) continue;
+      rc = run_conv(d, op, dtype, A, B, C, 0, ws, ws_bytes, stream, c, op == OP_DGRAD ? i : -1);  // warm-up
+      if (rc) break;
+      (void)hipEventRecord(e0, s);
+      for (int r = 0; r < reps; ++r)
+        rc = run_conv(d, op, dtype, A, B, C, 0, ws, ws_bytes, stream, c, op == OP_DGRAD ? i : -1);
+      (void)hipEventRecord(e1, s);
+      if (rc) break;
+      if (hipEventSynchronize(e1) != hipSuccess) { rc = fail(JR_ERR_HIP, "autotune: event sync failed"); break; }
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (ms < best_t) { best_t = ms; best_c = c; }
+    }
+    if (rc) break;
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    g_tuned[tune_key(op, M, N, K, d)] = best_c;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
   return rc;
 }
 
@@ -556,8 +789,8 @@ using namespace jr;
 
 JR_API size_t jr_conv2d_workspace_size(const jr_conv_desc* d, int op, int dtype) {
   (void)dtype;
-  if (!d || validate(d) != JR_OK) return 0;
-  return plan_ws_bytes(d, op);
+  if (!d || validate(d, op) != JR_OK) return 0;
+  return ws_bytes_for(d, op);
 }
 
 JR_API int jr_conv2d_fwd(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y,
@@ -573,4 +806,77 @@ JR_API int jr_conv2d_bwd_data(const jr_conv_desc* d, int dtype, const void* dy, 
 JR_API int jr_conv2d_bwd_filter(const jr_conv_desc* d, int dtype, const void* x, const void* dy,
                                 float* dw, void* ws, size_t ws_bytes, void* stream) {
   return run_conv(d, OP_WGRAD, dtype, x, dy, dw, 0, ws, ws_bytes, stream);
+}
+
+JR_API int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const void* a, const void* b, void* c,
+                              void* ws, size_t ws_bytes, void* stream) {
+  return autotune(d, op, dtype, a, b, c, ws, ws_bytes, stream, 3);
+}
+
+JR_API int jr_conv2d_num_configs(void) { return kNumCfgs; }
+
+// Diagnostic: time `reps` launches of one FWD GEMM of config `cfg` (0 or 3)
+// in variant dbg (0 normal, 1 no MFMA, 2 no DMA); returns ms via *ms.
+JR_API int jr_conv2d_debug_time(const jr_conv_desc* d, int cfg, int dbg, const void* x, const void* w, void* y,
+                                int reps, float* ms, void* stream) {
+  int rc = validate(d, OP_FWD);
+  if (rc) return rc;
+  ConvArgs a{};
+  fill_common(a, d);
+  a.A = (const float*)x; a.B = (const float*)w; a.C = (float*)y;
+  a.c_off = d->y_c_off; a.c_stride = d->y_c_stride;
+  Plan p = plan_for(d, OP_FWD, nullptr, cfg);
+  p.splits = 1; p.kt_per_split = p.ktiles;
+  a.M = p.M; a.N = p.N; a.K = p.K; a.ktiles = p.ktiles; a.kt_per_split = p.kt_per_split; a.ntn = p.nt;
+  hipStream_t s = as_stream(stream);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  dim3 grid(p.mt * p.nt, 1, 1);
+  (void)hipEventRecord(e0, s);
+  for (int r = 0; r < reps; ++r) {
+    if (cfg == 0) {
+      if (dbg == 0) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 128, 2, 16, 3, 0>), grid, dim3(256), 0, s, a);
+      if (dbg == 1) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 128, 2, 16, 3, 1>), grid, dim3(256), 0, s, a);
+      if (dbg == 2) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 128, 2, 16, 3, 2>), grid, dim3(256), 0, s, a);
+    } else {
+      if (dbg == 0) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 64, 2, 16, 4, 0>), grid, dim3(256), 0, s, a);
+      if (dbg == 1) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 64, 2, 16, 4, 1>), grid, dim3(256), 0, s, a);
+      if (dbg == 2) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 64, 2, 16, 4, 2>), grid, dim3(256), 0, s, a);
+    }
+  }
+  (void)hipEventRecord(e1, s);
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return check_launch("debug_time");
+}
+
+JR_API int jr_conv2d_set_config(const jr_conv_desc* d, int op, int phase, int cfg) {
+  int rc = validate(d, op);
+  if (rc) return rc;
+  if (cfg < 0 || cfg >= kNumCfgs) return fail(JR_ERR_INVALID, "conv set_config: bad config index");
+  Phase ph[64];
+  int nph = 1;
+  if (op == OP_DGRAD) {
+    dgrad_phases(d, ph, &nph);
+    if (phase < 0 || phase >= nph) return fail(JR_ERR_INVALID, "conv set_config: bad phase");
+  }
+  int M, N, K;
+  gemm_dims(d, op, op == OP_DGRAD ? &ph[phase] : nullptr, &M, &N, &K);
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tuned[tune_key(op, M, N, K, d)] = cfg;
+  return JR_OK;
+}
+
+JR_API int jr_conv2d_get_config(const jr_conv_desc* d, int op, int phase) {
+  if (!d || validate(d, op) != JR_OK) return -1;
+  Phase ph[64];
+  int nph = 1;
+  if (op == OP_DGRAD) {
+    dgrad_phases(d, ph, &nph);
+    if (phase < 0 || phase >= nph) return -1;
+  }
+  return plan_for(d, op, op == OP_DGRAD ? &ph[phase] : nullptr).cfg;
 }

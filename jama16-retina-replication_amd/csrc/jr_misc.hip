@@ -96,6 +96,17 @@ __global__ void k_u8_scale(const uint8_t* __restrict__ s, T* d, int64_t n) {
     Elt<T>::st(d + i, __fmul_rn((float)s[i], scale));
 }
 
+template <typename T>
+__global__ void k_image_u8(const uint8_t* __restrict__ s, T* d, int64_t pixels, int c, int ds) {
+  const float scale = 1.0f / 255.0f;
+  const int64_t total = pixels * ds;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i / ds;
+    const int ch = (int)(i - p * ds);
+    Elt<T>::st(d + i, ch < c ? __fmul_rn((float)s[p * c + ch], scale) : 0.f);
+  }
+}
+
 __global__ void k_brier(const float* __restrict__ p, const float* __restrict__ y, int n, double* acc) {
   __shared__ double red[256];
   const int t = threadIdx.x;
@@ -182,6 +193,22 @@ JR_API int jr_u8_to_f32_scaled(const uint8_t* src, void* dst, int dtype, int64_t
   else
     return fail(JR_ERR_INVALID, "u8_scale: bad dtype");
   return check_launch("u8_scale");
+}
+
+JR_API int jr_image_u8_to_nhwc(const uint8_t* src, void* dst, int dtype, int64_t pixels, int32_t c,
+                               int32_t dst_stride, void* stream) {
+  if (!src || !dst || pixels < 0 || c <= 0 || dst_stride < c) return fail(JR_ERR_INVALID, "image_u8: bad arguments");
+  if (pixels == 0) return JR_OK;
+  const int64_t n = pixels * dst_stride;
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_image_u8<float>, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), src, (float*)dst,
+                       pixels, c, dst_stride);
+  else if (dtype == JR_BF16)
+    hipLaunchKernelGGL(k_image_u8<uint16_t>, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), src,
+                       (uint16_t*)dst, pixels, c, dst_stride);
+  else
+    return fail(JR_ERR_INVALID, "image_u8: bad dtype");
+  return check_launch("image_u8");
 }
 
 JR_API int jr_brier_accumulate(const float* probs, const float* labels, int32_t n, double* acc, void* stream) {

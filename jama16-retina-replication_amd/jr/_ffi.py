@@ -52,6 +52,11 @@ _SIGS = {
                                    c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_bwd_filter": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_size_t, c_void_p]),
+    "jr_conv2d_autotune": (c_int, [POINTER(ConvDesc), c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_size_t, c_void_p]),
+    "jr_conv2d_get_config": (c_int, [POINTER(ConvDesc), c_int, c_int]),
+    "jr_conv2d_set_config": (c_int, [POINTER(ConvDesc), c_int, c_int, c_int]),
+    "jr_conv2d_num_configs": (c_int, []),
     "jr_bn_workspace_size": (c_size_t, [c_int64, c_int32]),
     "jr_bn_stats": (c_int, [c_int, c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
                             c_void_p, c_size_t, c_void_p]),
@@ -82,6 +87,7 @@ _SIGS = {
     "jr_cast_f32_to_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "jr_cast_bf16_to_f32": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "jr_u8_to_f32_scaled": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p]),
+    "jr_image_u8_to_nhwc": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int32, c_int32, c_void_p]),
     "jr_brier_accumulate": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "jr_graph_begin": (c_int, [c_void_p]),
     "jr_graph_end": (c_int, [c_void_p, POINTER(c_void_p)]),
@@ -124,7 +130,8 @@ def check(name: str, rc: int) -> None:
 def call(name: str, *args) -> int:
     lib = load()
     rc = getattr(lib, name)(*args)
-    if isinstance(rc, int) and name not in ("jr_conv2d_workspace_size", "jr_bn_workspace_size"):
+    if isinstance(rc, int) and name not in ("jr_conv2d_workspace_size", "jr_bn_workspace_size",
+                                            "jr_conv2d_get_config", "jr_conv2d_num_configs"):
         check(name, rc)
     return rc
 

@@ -39,7 +39,8 @@ class Engine:
     def __init__(self, batch: int, height: int = 299, width: int = 299, units: int = 1,
                  device: int | torch.device = 0, dtype: str = "f32", train: bool = True,
                  optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
-                 head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None):
+                 head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None,
+                 autotune: bool = True):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if dtype != "f32":
@@ -68,6 +69,8 @@ class Engine:
         self._calls: Dict[int, Tuple[list, list, list]] = {}
         self._graphs: Dict[int, int] = {}
         self.bucket_hooks: List[Tuple[int, Callable]] = []
+        if autotune:
+            self.autotune()
 
     # ------------------------------------------------------------------ memory
     def _t(self, n: int, dtype=torch.float32) -> torch.Tensor:
@@ -76,7 +79,11 @@ class Engine:
     def _alloc(self) -> None:
         g, B = self.g, self.batch
         fl = torch.float32
-        self.acts = [self._t(B * b.h * b.w * b.c, fl) for b in g.bufs]
+        # the image buffer is kept 4 channels wide (zero 4th channel): conv1's
+        # c_in = 3 runs on libjr's virtual channel padding
+        self.in_stride = (g.bufs[g.input_buf].c + 3) // 4 * 4
+        self.acts = [self._t(B * b.h * b.w * (self.in_stride if b.id == g.input_buf else b.c), fl)
+                     for b in g.bufs]
         self.raw = {n.idx: self._t(B * n.ho * n.wo * n.cout) for n in g.convs}
         self.stats = self._t(2 * sum(n.cout for n in g.convs))
         self.mean, self.invstd = {}, {}
@@ -113,6 +120,45 @@ class Engine:
         self.ws_bytes = int(ws)
         self.ws = self._t((self.ws_bytes + 15) // 4 + 4)
 
+    def autotune(self) -> None:
+        """jr_conv2d_autotune every conv op of the planned batch (cudnnFind
+        style: times each tile configuration on this engine's own buffers and
+        caches the fastest in libjr).  Runs before any data is loaded:
+        it overwrites raw / gradient buffers."""
+        L, B = self.lib, self.batch
+        ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
+        s = self._s
+        for n in self.g.convs:
+            d = self._conv_desc(n, B)
+            x = self.acts[n.x].data_ptr()
+            w = self._p(f"{n.name}/kernel")
+            _ffi.check("autotune fwd", L.jr_conv2d_autotune(ctypes.byref(d), _ffi.JR_CONV_FWD, self.dt, x, w,
+                                                             self.raw[n.idx].data_ptr(), ws, wsb, s))
+            if not self.train_mode:
+                continue
+            _ffi.check("autotune wgrad", L.jr_conv2d_autotune(
+                ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, self.dt, x, self.draw.data_ptr(),
+                self._gp(f"{n.name}/kernel"), ws, wsb, s))
+            if n.x != self.g.input_buf:
+                _ffi.check("autotune dgrad", L.jr_conv2d_autotune(
+                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.dt, self.draw.data_ptr(), w,
+                    self.dacts[n.x].data_ptr(), ws, wsb, s))
+        self.synchronize()
+        if self.train_mode:
+            self.grads.zero_()
+
+    def conv_configs(self) -> dict:
+        """{conv name: (fwd cfg, wgrad cfg, [dgrad cfg per phase])} in use."""
+        out = {}
+        for n in self.g.convs:
+            d = self._conv_desc(n, self.batch)
+            f = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_FWD, 0)
+            wg = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, 0)
+            dg = [self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, p)
+                  for p in range(n.stride * n.stride)]
+            out[n.name] = (f, wg, dg)
+        return out
+
     # ------------------------------------------------------------ parameters
     def load_params(self, flat: np.ndarray) -> None:
         flat = np.ascontiguousarray(flat, dtype=np.float32)
@@ -137,8 +183,9 @@ class Engine:
 
     # ------------------------------------------------------------ descriptors
     def _conv_desc(self, n: ConvNode, B: int) -> _ffi.ConvDesc:
+        xs = self.in_stride if n.x == self.g.input_buf else n.cin
         return _ffi.ConvDesc(B, n.h, n.w, n.cin, n.cout, n.kh, n.kw, n.stride, n.stride,
-                             n.pad_h, n.pad_w, n.ho, n.wo, 0, n.cin, 0, n.cout)
+                             n.pad_h, n.pad_w, n.ho, n.wo, 0, xs, 0, n.cout)
 
     def _pool_desc(self, n: PoolNode, B: int) -> _ffi.PoolDesc:
         yb = self.g.bufs[n.y.buf]
@@ -269,14 +316,17 @@ class Engine:
             raise ValueError(f"images must be [B,{ib.h},{ib.w},{ib.c}] NHWC, got {tuple(images.shape)}")
         with torch.cuda.stream(self.stream):
             x = torch.as_tensor(images)
+            pixels = B * ib.h * ib.w
             if x.dtype == torch.uint8:
                 xd = x.to(self.device, non_blocking=True).reshape(-1)
-                _ffi.check("jr_u8_to_f32_scaled", self.lib.jr_u8_to_f32_scaled(
-                    xd.data_ptr(), self.acts[self.g.input_buf].data_ptr(), self.dt, xd.numel(), self._s))
+                _ffi.check("jr_image_u8_to_nhwc", self.lib.jr_image_u8_to_nhwc(
+                    xd.data_ptr(), self.acts[self.g.input_buf].data_ptr(), self.dt, pixels, ib.c,
+                    self.in_stride, self._s))
                 self._keep_u8 = xd
             else:
-                self.acts[self.g.input_buf][:x.numel()].copy_(
-                    x.to(torch.float32).reshape(-1), non_blocking=True)
+                dst = self.acts[self.g.input_buf][:pixels * self.in_stride].view(pixels, self.in_stride)
+                dst[:, ib.c:].zero_()
+                dst[:, :ib.c].copy_(x.to(torch.float32).reshape(pixels, ib.c), non_blocking=True)
             if labels is not None:
                 y = torch.as_tensor(labels, dtype=torch.float32).reshape(-1)
                 if y.numel() != B * self.units:

@@ -84,9 +84,12 @@ def test_conv_fwd_dgrad_wgrad(case):
     rng = np.random.default_rng(hash(case) % 2**31)
     x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
     wt = (rng.standard_normal((kh, kw, cin, cout)) / np.sqrt(kh * kw * cin)).astype(np.float32)
-    d, ho, wo = _desc(ffi, n, h, w, cin, cout, kh, kw, s, pad)
+    cs = (cin + 3) // 4 * 4          # c_in % 4 != 0: input kept 4-aligned, zero padded
+    d, ho, wo = _desc(ffi, n, h, w, cin, cout, kh, kw, s, pad, x_stride=cs)
     ref = R.conv2d(x, wt, s, pad)
-    X, W = dev(x), dev(wt)
+    xp = np.zeros((n, h, w, cs), np.float32)
+    xp[..., :cin] = x
+    X, W = dev(xp), dev(wt)
     Y = torch.zeros(n * ho * wo * cout, device="cuda")
     ws, wsb = _ws(ffi, d, 0)
     ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), 0, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
@@ -116,6 +119,47 @@ def test_conv_fwd_dgrad_wgrad(case):
                                               ws.data_ptr(), wsb, None))
     got = host(DW).reshape(wt.shape)
     assert relerr(got, ref_dw) < 1e-5, relerr(got, ref_dw)
+
+
+@pytest.mark.parametrize("case", [(2, 17, 17, 64, 96, 3, 3, 1, "same"), (2, 17, 17, 48, 64, 3, 3, 2, "valid"),
+                                  (2, 11, 11, 3, 32, 3, 3, 2, "valid")])
+def test_conv_every_tile_config(case):
+    """Every tile configuration the autotuner may pick is correct."""
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, cin, cout, kh, kw, s, pad = case
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
+    wt = (rng.standard_normal((kh, kw, cin, cout)) / np.sqrt(kh * kw * cin)).astype(np.float32)
+    cs = (cin + 3) // 4 * 4
+    xp = np.zeros((n, h, w, cs), np.float32)
+    xp[..., :cin] = x
+    d, ho, wo = _desc(ffi, n, h, w, cin, cout, kh, kw, s, pad, x_stride=cs)
+    ref = R.conv2d(x, wt, s, pad)
+    dy = rng.standard_normal(ref.shape).astype(np.float32)
+    ref_dx = R.conv2d_bwd_data(dy, wt, x.shape, s, pad) if cin % 4 == 0 else None
+    ref_dw = R.conv2d_bwd_filter(x, dy, wt.shape, s, pad)
+    X, W, DY = dev(xp), dev(wt), dev(dy)
+    wsb = max(L.jr_conv2d_workspace_size(ctypes.byref(d), op, 0) for op in range(3))
+    ws = torch.zeros(wsb // 4 + 4, device="cuda")
+    for cfg in range(L.jr_conv2d_num_configs()):
+        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, 0, cfg))
+        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 2, 0, cfg))
+        Y = torch.zeros(ref.size, device="cuda")
+        ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), 0, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
+                                         ws.data_ptr(), wsb, None))
+        assert relerr(host(Y).reshape(ref.shape), ref) < 5e-6, cfg
+        DW = torch.zeros(wt.size, device="cuda")
+        ffi.check("wgrad", L.jr_conv2d_bwd_filter(ctypes.byref(d), 0, X.data_ptr(), DY.data_ptr(), DW.data_ptr(),
+                                                  ws.data_ptr(), wsb, None))
+        assert relerr(host(DW).reshape(wt.shape), ref_dw) < 1e-5, cfg
+        if ref_dx is not None:
+            for ph in range(s * s):
+                ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 1, ph, cfg))
+            DX = torch.zeros(x.size, device="cuda")
+            ffi.check("dgrad", L.jr_conv2d_bwd_data(ctypes.byref(d), 0, DY.data_ptr(), W.data_ptr(), DX.data_ptr(),
+                                                    0, ws.data_ptr(), wsb, None))
+            assert relerr(host(DX).reshape(x.shape), ref_dx) < 5e-6, cfg
 
 
 def test_conv_channel_slices():

@@ -13,12 +13,13 @@ seq = [(n, "fwd") for n in g.convs]
 for n in reversed(g.convs):
     seq.append((n, "wgrad"))
     if n.idx != 0:
-        seq.append((n, "dgrad"))
+        for ph in range(n.stride * n.stride):   # one GEMM per stride phase
+            seq.append((n, "dgrad" if n.stride == 1 else f"dg{ph}"))
 conv = []
 i = 0
 while i < len(rows):
     r = rows[i]
-    if "k_conv_f32" in r["Kernel_Name"]:
+    if "k_conv" in r["Kernel_Name"] and "splitk" not in r["Kernel_Name"]:
         t = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         j = i + 1
         if j < len(rows) and "splitk_reduce" in rows[j]["Kernel_Name"]:
@@ -31,7 +32,7 @@ last = conv[-len(seq):]
 tot_t = 0; tot_f = 0
 out = []
 for (n, op), (r, t, t2) in zip(seq, last):
-    f = 2 * n.macs_per_image() * B
+    f = 2 * n.macs_per_image() * B / (n.stride * n.stride if op.startswith("dg") and op != "dgrad" else 1)
     tot_t += t + t2; tot_f += f
     name = r["Kernel_Name"]; cfg = name[name.index("<"):name.index(">") + 1]
     out.append((t + t2, f"{n.name:10s} {op:5s} {n.kh}x{n.kw}/{n.stride} {n.h:3d}x{n.w:<3d} {n.cin:4d}->{n.cout:4d} "

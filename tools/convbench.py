@@ -1,0 +1,32 @@
+"""Diagnostic: time one conv fwd GEMM (conv5 shape) in normal / no-MFMA /
+no-DMA variants to see which side bounds the kernel."""
+import ctypes, os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "jama16-retina-replication_amd"))
+import torch
+from jr import _ffi
+_ffi.init(0)
+L = _ffi.load()
+L.jr_conv2d_debug_time.restype = ctypes.c_int
+L.jr_conv2d_debug_time.argtypes = [ctypes.POINTER(_ffi.ConvDesc), ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                                   ctypes.c_void_p]
+cases = {"conv5 73x73 80->192 3x3": (64, 73, 73, 80, 192, 3, 3, 1, 0),
+         "mixed 35x35 288->64 1x1": (64, 35, 35, 288, 64, 1, 1, 1, 0),
+         "gemm-like 17x17 768->192 1x1": (64, 17, 17, 768, 192, 1, 1, 1, 0),
+         "mixed10 8x8 448->384 3x3": (64, 8, 8, 448, 384, 3, 3, 1, 1)}
+for name, (n, h, w, ci, co, kh, kw, s, p) in cases.items():
+    ho, wo = (h + 2 * p - kh) // s + 1, (w + 2 * p - kw) // s + 1
+    d = _ffi.ConvDesc(n, h, w, ci, co, kh, kw, s, s, p, p, ho, wo, 0, ci, 0, co)
+    x = torch.randn(n * h * w * ci, device="cuda")
+    wt = torch.randn(kh * kw * ci * co, device="cuda") * 0.05
+    y = torch.zeros(n * ho * wo * co, device="cuda")
+    flops = 2.0 * n * ho * wo * co * kh * kw * ci
+    for cfg in (0, 3):
+        res = []
+        for dbg in (0, 1, 2):
+            ms = ctypes.c_float()
+            L.jr_conv2d_debug_time(ctypes.byref(d), cfg, dbg, x.data_ptr(), wt.data_ptr(), y.data_ptr(), 2, ctypes.byref(ms), None)
+            L.jr_conv2d_debug_time(ctypes.byref(d), cfg, dbg, x.data_ptr(), wt.data_ptr(), y.data_ptr(), 10, ctypes.byref(ms), None)
+            t = ms.value / 10
+            res.append(f"dbg{dbg}: {t*1e3:8.1f}us {flops/t/1e9:6.1f}TF")
+        print(f"{name:32s} cfg{cfg}: " + " | ".join(res), flush=True)
