@@ -179,6 +179,11 @@ int jr_image_u8_to_nhwc(const uint8_t* src, void* dst, int dtype, int64_t pixels
  * train.py:175-177) */
 int jr_brier_accumulate(const float* probs, const float* labels, int32_t n, double* acc, void* stream);
 
+/* ---- host (CPU) helpers: TFRecord container checksums -------------- */
+uint32_t jr_crc32c(const uint8_t* data, size_t n, uint32_t crc);
+/* TFRecord masked CRC32C: ((c >> 15) | (c << 17)) + 0xa282ead8 */
+uint32_t jr_masked_crc32c(const uint8_t* data, size_t n);
+
 /* ---- HIP graph capture of a whole step ------------------------------ */
 int jr_graph_begin(void* stream);
 int jr_graph_end(void* stream, void** graph_exec);

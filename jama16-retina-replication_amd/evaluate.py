@@ -1,0 +1,212 @@
+"""Drop-in for the reference's evaluate.py: same flags, model-path expansion
+(comma list or glob), linear ensemble average, metrics, printed lines and
+CSV; inference runs on libjr (MI355X).
+
+  python evaluate.py (-e | -m | -o --data_dir D) [-lm PATHS] [-so CSV] [-b 32] [-op 0.5]
+Multi-GPU: torchrun --nproc-per-node N evaluate.py ... shards whole batches
+(dataset order, so every BN batch is the reference's, App. C Q1) across
+ranks with no collective on the data path; rank 0 gathers the [N] per-model
+predictions, averages and scores them.
+"""
+import argparse
+import csv
+import os
+import random
+import sys
+from glob import glob
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import lib.dataset  # noqa: E402
+import lib.evaluation  # noqa: E402
+import lib.metrics  # noqa: E402
+
+# evaluate.py:24-29
+DEFAULT_EYEPACS_DIR = "./data/eyepacs/bin2/test"
+DEFAULT_MESSIDOR_DIR = "./data/messidor/bin2"
+DEFAULT_LOAD_MODEL_PATH = "./tmp/model"
+DEFAULT_SAVE_OPERATING_THRESHOLDS_PATH = "./tmp/test_op_pts.csv"
+DEFAULT_BATCH_SIZE = 32
+
+# evaluate.py:96-101
+NUM_CHANNELS = 3
+NUM_WORKERS = 8
+NUM_THRESHOLDS = 200
+KEPSILON = 1e-7
+
+
+def build_parser():
+    p = argparse.ArgumentParser(
+        description="Evaluate performance of trained graph on test data set. "
+                    "Specify --data_dir if you use the -o param.")
+    p.add_argument("-m", "--messidor", action="store_true", help="evaluate performance on Messidor-Original")
+    p.add_argument("-e", "--eyepacs", action="store_true", help="evaluate performance on EyePacs set")
+    p.add_argument("-o", "--other", action="store_true", help="evaluate performance on your own dataset")
+    p.add_argument("--data_dir", help="directory where data set resides")
+    p.add_argument("-lm", "--load_model_path", default=DEFAULT_LOAD_MODEL_PATH,
+                   help="path to where graph model should be loaded from creates an ensemble if paths are "
+                        "comma separated or a regexp")
+    p.add_argument("-so", "--save_operating_thresholds_path", default=DEFAULT_SAVE_OPERATING_THRESHOLDS_PATH,
+                   help="path to where operating points metrics should be saved")
+    p.add_argument("-b", "--batch_size", default=DEFAULT_BATCH_SIZE, help="batch size")
+    p.add_argument("-op", "--operating_threshold", default=0.5, help="operating threshold")
+    return p
+
+
+def expand_model_paths(load_model_path: str):
+    """evaluate.py:74-83: comma list, or glob when the path holds '*', '+'
+    or '?' (each match's last extension stripped, duplicates removed)."""
+    if "," in load_model_path:
+        return load_model_path.split(",")
+    if any(ch in load_model_path for ch in "*+?"):
+        stems = {".".join(x.split(".")[:-1]) for x in glob("{}*".format(load_model_path))}
+        return sorted(stems)
+    return [load_model_path]
+
+
+def predict_all(engine, paths, data_dir, batch_size, rank=0, world=1):
+    """Per-model predictions over this rank's batches: ([M][n_r, 1], [n_r, 1],
+    batch indices)."""
+    from jr import checkpoint
+    from jr.session import Session
+    sess = Session(engine)
+    dataset = lib.dataset.initialize_dataset(
+        data_dir, batch_size, num_workers=NUM_WORKERS, prefetch_buffer_size=2 * batch_size,
+        image_data_format="channels_last", num_channels=NUM_CHANNELS,
+        image_dim=[engine.g.height, engine.g.width], decode_dtype="uint8")
+    preds, labels, order = [], None, None
+    for path in paths:
+        flat, _ = checkpoint.load(path, engine.g)
+        engine.load_params(flat)
+        got_y = []
+        ids = []
+
+        def feed(it=iter(enumerate(dataset))):
+            while True:
+                i, (x, y) = next(it)
+                if i % world == rank:
+                    ids.append(i)
+                    got_y.append(y)
+                    return {"x": x, "y": y}
+
+        out = lib.evaluation.perform_test(sess=sess, init_op=None, feed_dict_fn=feed,
+                                          custom_tensors=["predictions"])
+        preds.append(out[0])
+        if labels is None:                 # labels from the first model (evaluate.py:116-117,211)
+            labels = np.vstack(got_y) if got_y else np.zeros((0, 1), np.float32)
+            order = list(ids)
+    return preds, labels, order
+
+
+def main(argv=None):
+    parser = build_parser()
+    args = parser.parse_args(argv)
+    # evaluate.py:53-56 (chained comparison kept as is, App. C Q5)
+    if bool(args.eyepacs) == bool(args.messidor) == bool(args.other):
+        print("Can only evaluate one data set at once!")
+        parser.print_help()
+        return 2
+    if args.data_dir is not None:
+        data_dir = str(args.data_dir)
+    elif args.eyepacs:
+        data_dir = DEFAULT_EYEPACS_DIR
+    elif args.messidor:
+        data_dir = DEFAULT_MESSIDOR_DIR
+    else:
+        print("Please specify --data_dir.")
+        parser.print_help()
+        return 2
+
+    import torch
+    from jr import checkpoint
+    from jr.engine import Engine
+
+    load_model_paths = expand_model_paths(str(args.load_model_path))
+    batch_size = int(args.batch_size)
+    operating_threshold = float(args.operating_threshold)
+    save_path = str(args.save_operating_thresholds_path)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    print(f"Numpy version: {np.__version__}")
+    print(f"Torch version: {torch.__version__} (libjr / MI355X backend)")
+    random.seed(432)
+    if rank == 0:
+        print("""
+Evaluating: {},
+Saving operating thresholds metrics at: {},
+Using operating treshold: {},
+""".format(data_dir, save_path, operating_threshold))
+        print("Trying to load model(s):\n{}".format("\n".join(load_model_paths)))
+
+    thresholds = lib.metrics.generate_thresholds(NUM_THRESHOLDS, KEPSILON) + [operating_threshold]
+    _, meta = checkpoint.load(load_model_paths[0])
+    engine = Engine(batch_size, meta["height"], meta["width"], meta.get("units", 1), device=local,
+                    train=False)
+    preds, labels, order = predict_all(engine, load_model_paths, data_dir, batch_size, rank, world)
+
+    if dist:   # gather every rank's batches to rank 0, restore dataset order
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (order, preds, labels))
+        if rank != 0:
+            dist.destroy_process_group()
+            return 0
+        pieces = []
+        for o, p, y in gathered:
+            sizes = np.cumsum([0] + [batch_size] * len(o))
+            # the last batch may be partial
+            if len(o) and y.shape[0] < sizes[-1]:
+                sizes[-1] = y.shape[0]
+            for k, bi in enumerate(o):
+                pieces.append((bi, [m[sizes[k]:sizes[k + 1]] for m in p], y[sizes[k]:sizes[k + 1]]))
+        pieces.sort(key=lambda t: t[0])
+        preds = [np.vstack([pc[1][m] for pc in pieces]) for m in range(len(load_model_paths))]
+        labels = np.vstack([pc[2] for pc in pieces])
+
+    all_predictions = np.array(preds)
+    avg_pred = np.mean(all_predictions, axis=0)          # evaluate.py:214-217
+    all_y = labels
+
+    names = {"tp": lib.metrics.true_positives_at_thresholds, "fp": lib.metrics.false_positives_at_thresholds,
+             "fn": lib.metrics.false_negatives_at_thresholds, "tn": lib.metrics.true_negatives_at_thresholds}
+    state = {k: lib.metrics.create_reset_metric(f, scope=k, thresholds=thresholds) for k, f in names.items()}
+    state["brier"] = lib.metrics.create_reset_metric(lib.metrics.mean_squared_error, scope="brier")
+    state["auc"] = lib.metrics.create_reset_metric(lib.metrics.auc, scope="auc")
+    for value, update, reset in state.values():
+        reset()
+        update(all_y, avg_pred)
+    tp, fp, fn, tn = (state[k][0]() for k in ("tp", "fp", "fn", "tn"))
+    test_conf_matrix = lib.metrics.confusion_matrix(tp[-1], fp[-1], fn[-1], tn[-1])
+    test_brier, test_auc = state["brier"][0](), state["auc"][0]()
+    test_specificities = tn / (tn + fp + np.float32(KEPSILON))
+    test_sensitivities = tp / (tp + fn + np.float32(KEPSILON))
+
+    print(f"Brier score: {test_brier:6.4}, AUC: {test_auc:10.8}")
+    print(f"Confusion matrix at operating threshold {operating_threshold:0.3f}")
+    print(test_conf_matrix[0])
+    print("Specificity: {0:0.4f}, Sensitivity: {1:0.4f} at Operating Threshold {2:0.4f}.".format(
+        test_specificities[-1], test_sensitivities[-1], thresholds[-1]))
+    os.makedirs(os.path.dirname(os.path.abspath(save_path)), exist_ok=True)
+    with open(save_path, "w") as f:
+        w = csv.writer(f, delimiter=" ")
+        w.writerow(["threshold", "specificity", "sensitivity"])
+        for idx in range(NUM_THRESHOLDS):
+            w.writerow(["{:0.4f}".format(v) for v in (thresholds[idx], test_specificities[idx],
+                                                       test_sensitivities[idx])])
+    if dist:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -89,6 +89,8 @@ _SIGS = {
     "jr_u8_to_f32_scaled": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p]),
     "jr_image_u8_to_nhwc": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int32, c_int32, c_void_p]),
     "jr_brier_accumulate": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "jr_crc32c": (ctypes.c_uint32, [c_void_p, c_size_t, ctypes.c_uint32]),
+    "jr_masked_crc32c": (ctypes.c_uint32, [c_void_p, c_size_t]),
     "jr_graph_begin": (c_int, [c_void_p]),
     "jr_graph_end": (c_int, [c_void_p, POINTER(c_void_p)]),
     "jr_graph_launch": (c_int, [c_void_p, c_void_p]),

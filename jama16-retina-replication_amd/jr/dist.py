@@ -21,6 +21,7 @@ gradient.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import List, Tuple
 
 import torch
@@ -63,11 +64,15 @@ class BucketAllReduce:
         self.works = []
         self.next = 0
 
+    def _stream_ctx(self):
+        s = getattr(self.eng, "stream", None)
+        return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
+
     def _issue_ready(self, ready_from: int) -> None:
         eng = self.eng
         while self.next < len(self.buckets) and self.buckets[self.next][0] >= ready_from:
             lo, hi = self.buckets[self.next]
-            with torch.cuda.stream(eng.stream):
+            with self._stream_ctx():
                 w = dist.all_reduce(eng.grads[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             self.works.append(w)
             self.next += 1
@@ -79,7 +84,7 @@ class BucketAllReduce:
 
     def finish(self, eng=None) -> float:
         self._issue_ready(0)
-        with torch.cuda.stream(self.eng.stream):
+        with self._stream_ctx():
             for w in self.works:
                 w.wait()
         self.works = []

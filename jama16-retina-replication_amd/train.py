@@ -1,0 +1,215 @@
+"""Drop-in for the reference's train.py: same flags, constants, printed lines,
+checkpoints and operating-point CSV; the graph/session machinery is replaced
+by jr (libjr HIP kernels on MI355X).
+
+  python train.py [-t TRAIN_DIR] [-v VAL_DIR] [-sm SAVE_MODEL_PATH]
+                  [-ss SAVE_SUMMARIES_DIR] [-so SAVE_OPERATING_THRESHOLDS_PATH]
+                  [-sgd]
+Multi-GPU (data parallel, RCCL): torchrun --nproc-per-node N train.py ...
+Reference behaviour kept: BN uses batch statistics in
+training and validation (Q1); weights start from Keras default init (Q2);
+images are channels_last (Q3: the reference's channels_first path is a
+reshape that scrambles pixels, so it is not reproduced).
+"""
+import argparse
+import csv
+import os
+import random
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import lib.dataset  # noqa: E402
+import lib.evaluation  # noqa: E402
+import lib.metrics  # noqa: E402
+
+# train.py:19-24
+DEFAULT_TRAIN_DIR = "./data/eyepacs/bin2/train"
+DEFAULT_VAL_DIR = "./data/eyepacs/bin2/validation"
+DEFAULT_SAVE_MODEL_PATH = "./tmp/model"
+DEFAULT_SAVE_SUMMARIES_DIR = "./tmp/logs"
+DEFAULT_SAVE_OPERATING_THRESHOLDS_PATH = "./tmp/op_pts.csv"
+
+# train.py:66-89
+NUM_CHANNELS = 3
+NUM_WORKERS = 8
+LEARNING_RATE = 3e-3
+MOMENTUM = 0.9
+USE_NESTEROV = True
+TRAIN_BATCH_SIZE = 64
+NUM_EPOCHS = 200
+WAIT_EPOCHS = 10
+MIN_DELTA_AUC = 0.01
+VAL_BATCH_SIZE = 64
+NUM_THRESHOLDS = 200
+KEPSILON = 1e-7
+SHUFFLE_BUFFER_SIZE = 2048
+
+
+def build_parser():
+    p = argparse.ArgumentParser(
+        description="Trains and saves neural network for detection of diabetic retinopathy.")
+    p.add_argument("-t", "--train_dir", default=DEFAULT_TRAIN_DIR,
+                   help="path to folder that contains training tfrecords")
+    p.add_argument("-v", "--val_dir", default=DEFAULT_VAL_DIR,
+                   help="path to folder that contains validation tfrecords")
+    p.add_argument("-sm", "--save_model_path", default=DEFAULT_SAVE_MODEL_PATH,
+                   help="path to where graph model should be saved")
+    p.add_argument("-ss", "--save_summaries_dir", default=DEFAULT_SAVE_SUMMARIES_DIR,
+                   help="path to folder where summaries should be saved")
+    p.add_argument("-so", "--save_operating_thresholds_path", default=DEFAULT_SAVE_OPERATING_THRESHOLDS_PATH,
+                   help="path to where operating points should be saved")
+    p.add_argument("-sgd", "--vanilla_sgd", action="store_true",
+                   help="use vanilla stochastic gradient descent instead of "
+                        "nesterov accelerated gradient descent")
+    # extras (not in the reference): resolution, epochs, seeds, device
+    p.add_argument("--image_size", type=int, default=299, help="input resolution (299; 587 high-res variant)")
+    p.add_argument("--num_epochs", type=int, default=NUM_EPOCHS)
+    p.add_argument("--seed", type=int, default=0, help="weight init seed (ensemble member index)")
+    p.add_argument("--shuffle_seed", type=int, default=None)
+    p.add_argument("--max_steps_per_epoch", type=int, default=None)
+    return p
+
+
+def status_line(epoch, num_epochs, batch_num, xent, i_step=None):
+    """train.py:191-203: one \\r-terminated status line."""
+    width = len(str(num_epochs))
+    parts = [f"Epoch: {epoch:>{width}}/{num_epochs:>{width}}", f"Batch: {batch_num:>4}, Xent: {xent:6.4}"]
+    if i_step is not None:
+        parts.append(f"Step: {i_step:>10}")
+    return ", ".join(parts)
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    import torch
+    from jr import checkpoint
+    from jr.engine import Engine
+    from jr.session import Session
+    from jr.summary import FileWriter
+
+    print(f"Numpy version: {np.__version__}")
+    print(f"Torch version: {torch.__version__} (libjr / MI355X backend)")
+    random.seed(432)                       # train.py:17
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    if rank == 0:
+        print(f"""
+Training images folder: {args.train_dir},
+Validation images folder: {args.val_dir},
+Saving model and graph checkpoints at: {args.save_model_path},
+Saving summaries at: {args.save_summaries_dir},
+Saving operating points at: {args.save_operating_thresholds_path},
+Use SGD: {bool(args.vanilla_sgd)}
+""")
+
+    thresholds = lib.metrics.generate_thresholds(NUM_THRESHOLDS, KEPSILON) + [0.5]
+    size = [args.image_size, args.image_size]
+    shuffle_seed = args.shuffle_seed if args.shuffle_seed is not None else int.from_bytes(os.urandom(4), "little")
+    if dist:   # every rank walks the same shuffled stream and takes its batches
+        t = torch.tensor([shuffle_seed], dtype=torch.int64, device="cuda")
+        dist.broadcast(t, 0)
+        shuffle_seed = int(t.item())
+    train_dataset = lib.dataset.initialize_dataset(
+        args.train_dir, TRAIN_BATCH_SIZE, num_workers=NUM_WORKERS,
+        prefetch_buffer_size=2 * TRAIN_BATCH_SIZE, shuffle_buffer_size=SHUFFLE_BUFFER_SIZE,
+        image_data_format="channels_last", num_channels=NUM_CHANNELS, image_dim=size,
+        seed=shuffle_seed, decode_dtype="uint8")
+    val_dataset = lib.dataset.initialize_dataset(
+        args.val_dir, VAL_BATCH_SIZE, num_workers=NUM_WORKERS,
+        prefetch_buffer_size=2 * TRAIN_BATCH_SIZE, shuffle_buffer_size=SHUFFLE_BUFFER_SIZE,
+        image_data_format="channels_last", num_channels=NUM_CHANNELS, image_dim=size,
+        seed=shuffle_seed + 1, decode_dtype="uint8")
+
+    engine = Engine(max(TRAIN_BATCH_SIZE, VAL_BATCH_SIZE), args.image_size, args.image_size,
+                    device=local, optimizer="sgd" if args.vanilla_sgd else ("nesterov" if USE_NESTEROV else "momentum"),
+                    lr=LEARNING_RATE, momentum=MOMENTUM, seed=args.seed)
+    sess = Session(engine, thresholds, NUM_THRESHOLDS, KEPSILON)
+    if dist:
+        from jr.dist import BucketAllReduce
+        sess.allreduce = BucketAllReduce(engine, world)
+        sess.shard = (rank, world)
+    train_writer = FileWriter(os.path.join(args.save_summaries_dir, "train")) if rank == 0 else None
+
+    latest_peak_auc = 0.0
+    waited_epochs = 0
+    saved = False
+    steps_per_epoch = None
+    if dist:
+        n_batches = -(-train_dataset.num_records() // TRAIN_BATCH_SIZE)
+        steps_per_epoch = n_batches // world
+    for epoch in range(args.num_epochs):
+        sess.reset("brier")
+        batch_num = 0
+        for i, (images, labels) in enumerate(train_dataset):
+            if dist and i % world != rank:
+                continue
+            if steps_per_epoch is not None and batch_num >= steps_per_epoch:
+                break
+            if args.max_steps_per_epoch is not None and batch_num >= args.max_steps_per_epoch:
+                break
+            i_global, xent, probs = sess.train_batch(images, labels)
+            sess.update(labels, probs, "brier")
+            if rank == 0:
+                print(status_line(epoch, args.num_epochs, batch_num, xent, i_global), end="\r")
+            batch_num += 1
+        train_brier = sess.value("brier")
+        if rank == 0:
+            print("\nEnd of epoch {0}! (Brier: {1:8.6})".format(epoch, train_brier))
+
+        val_auc = lib.evaluation.perform_test(sess=sess, init_op=val_dataset,
+                                              summary_writer=train_writer, epoch=epoch)
+        if val_auc < latest_peak_auc + MIN_DELTA_AUC:
+            if WAIT_EPOCHS == waited_epochs:
+                if rank == 0:
+                    print("Stopped early at epoch {0} with saved peak auc {1:10.8}".format(epoch + 1, latest_peak_auc))
+                break
+            waited_epochs += 1
+        else:
+            latest_peak_auc = val_auc
+            if rank == 0:
+                print(f"New peak auc reached: {val_auc:10.8}")
+                checkpoint.save(args.save_model_path, engine.g, engine.params_numpy(),
+                                {"epoch": epoch, "val_auc": float(val_auc)})
+            saved = True
+            waited_epochs = 0
+
+    # train.py:272-300: restore the best weights, sweep the training set,
+    # write specificity/sensitivity per threshold.
+    if dist:
+        dist.barrier()
+    if saved:
+        flat, _ = checkpoint.load(args.save_model_path, engine.g)
+        engine.load_params(flat)
+    sess.reset("tp", "fp", "fn", "tn")
+    for images, labels in train_dataset:
+        probs = sess.predict(images, labels)
+        sess.update(labels, probs, "tp", "fp", "fn", "tn")
+    if rank == 0:
+        os.makedirs(os.path.dirname(os.path.abspath(args.save_operating_thresholds_path)), exist_ok=True)
+        spec, sens = sess.specificities(), sess.sensitivities()
+        with open(args.save_operating_thresholds_path, "w") as f:
+            w = csv.writer(f, delimiter=" ")
+            w.writerow(["threshold", "specificity", "sensitivity"])
+            for idx in range(NUM_THRESHOLDS):
+                w.writerow(["{:0.4f}".format(v) for v in (thresholds[idx], spec[idx], sens[idx])])
+    if train_writer:
+        train_writer.close()
+    if dist:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

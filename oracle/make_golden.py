@@ -1,0 +1,152 @@
+"""Generate the committed golden fixtures under tests/golden/ (TEST ORACLE).
+
+Parity status: UNPINNED — the reference (TF 1.x) cannot run here and ships no
+vectors (oracle/__init__.py).  These fixtures freeze the oracle's own outputs
+(numpy fp64 per op, torch-CPU fp64 for the whole network) so that
+  * CPU tests can check the oracle against them (regression, and the torch
+    cross-formulation), and
+  * GPU tests on the box (where /root/reference and this generator's time
+    budget are absent) compare libjr against fixed expected values.
+Weights are NOT stored: they are regenerated from the seed by jr.init
+(numpy PCG64), inputs from jr.synth (PCG64(432 + i)).
+
+  python oracle/make_golden.py [--only ops,metrics,net107,net299,curve]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "jama16-retina-replication_amd"))
+OUT = os.path.join(ROOT, "tests", "golden")
+
+from oracle import metrics_ref as MR  # noqa: E402
+from oracle import tf_ops as R  # noqa: E402
+
+CONV_GOLDEN = [  # n, h, w, cin, cout, kh, kw, stride, padding
+    (2, 9, 9, 8, 16, 3, 3, 1, "same"),
+    (2, 11, 11, 8, 16, 3, 3, 2, "valid"),
+    (1, 7, 8, 4, 16, 1, 7, 1, "same"),
+    (1, 8, 7, 4, 16, 7, 1, 1, "same"),
+    (2, 9, 9, 3, 16, 3, 3, 2, "valid"),
+    (1, 6, 6, 12, 16, 5, 5, 1, "same"),
+]
+
+
+def ops():
+    rng = np.random.default_rng(20261015)
+    d = {}
+    for i, (n, h, w, ci, co, kh, kw, s, p) in enumerate(CONV_GOLDEN):
+        x = rng.standard_normal((n, h, w, ci)).astype(np.float32)
+        wt = (rng.standard_normal((kh, kw, ci, co)) / np.sqrt(kh * kw * ci)).astype(np.float32)
+        y = R.conv2d(x, wt, s, p)
+        dy = rng.standard_normal(y.shape).astype(np.float32)
+        d[f"conv{i}_x"], d[f"conv{i}_w"], d[f"conv{i}_dy"] = x, wt, dy
+        d[f"conv{i}_y"] = y
+        d[f"conv{i}_dx"] = R.conv2d_bwd_data(dy, wt, x.shape, s, p)
+        d[f"conv{i}_dw"] = R.conv2d_bwd_filter(x, dy, wt.shape, s, p)
+    x = (rng.standard_normal((3, 5, 5, 8)) * 2 + 1).astype(np.float32)
+    beta = rng.standard_normal(8).astype(np.float32) * 0.3
+    dy = rng.standard_normal(x.shape).astype(np.float32)
+    d["bn_x"], d["bn_beta"], d["bn_dy"] = x, beta, dy
+    d["bn_y"], d["bn_mean"], d["bn_invstd"] = R.bn_relu_fwd(x, beta)
+    d["bn_dx"], d["bn_dbeta"] = R.bn_relu_bwd(dy, x, beta)
+    x = np.maximum(rng.standard_normal((2, 9, 11, 4)), 0).astype(np.float32)
+    d["mp_x"] = x
+    d["mp_y"], d["mp_arg"] = R.maxpool3x3s2(x)
+    d["mp_dy"] = rng.standard_normal(d["mp_y"].shape).astype(np.float32)
+    d["mp_dx"] = R.maxpool3x3s2_bwd(d["mp_dy"], d["mp_arg"], x.shape)
+    x = rng.standard_normal((2, 4, 6, 4)).astype(np.float32)
+    d["ap_x"], d["ap_y"] = x, R.avgpool3x3s1_same(x)
+    d["ap_dy"] = rng.standard_normal(x.shape).astype(np.float32)
+    d["ap_dx"] = R.avgpool3x3s1_same_bwd(d["ap_dy"])
+    f = rng.standard_normal((6, 16)).astype(np.float32)
+    W = rng.standard_normal((16, 1)).astype(np.float32) * 0.3
+    b = np.array([0.2], np.float32)
+    y = (rng.random((6, 1)) < 0.4).astype(np.float32)
+    z = R.dense(f, W, b)
+    d.update(head_f=f, head_w=W, head_b=b, head_y=y, head_z=z, head_p=R.sigmoid(z),
+             head_loss=np.array(R.sigmoid_xent_mean(z, y)), head_dz=R.sigmoid_xent_grad(z, y))
+    w0, g0, a0 = (rng.standard_normal(10).astype(np.float32) for _ in range(3))
+    w1, a1 = R.nesterov(w0.astype(np.float64), g0, a0)
+    d.update(nest_w=w0, nest_g=g0, nest_a=a0, nest_w1=w1, nest_a1=a1)
+    u8 = np.arange(256, dtype=np.uint8)
+    d["u8"], d["u8_scaled"] = u8, R.convert_image_dtype_u8(u8)
+    np.savez_compressed(os.path.join(OUT, "ops_small.npz"), **d)
+
+
+def metrics():
+    rng = np.random.default_rng(7)
+    n = 1000
+    y = (rng.random((n, 1)) < 0.3).astype(np.float32)
+    p = np.clip(0.5 * rng.random((n, 1)) + 0.4 * y, 0, 1).astype(np.float32)
+    thr = MR.generate_thresholds(200, 1e-7) + [0.5]
+    tp, fp, fn, tn = MR.counts_at_thresholds(y, p, thr)
+    spec, sens = MR.spec_sens(tp, fp, fn, tn)
+    np.savez_compressed(os.path.join(OUT, "metrics.npz"), labels=y, preds=p, thresholds=np.array(thr),
+                        tp=tp, fp=fp, fn=fn, tn=tn, spec=spec, sens=sens,
+                        auc=np.array(MR.auc(y, p)), brier=np.array(MR.brier(y, p)),
+                        confusion=MR.confusion_matrix(tp[-1], fp[-1], fn[-1], tn[-1]))
+
+
+def _net(res, batch, seed, steps=1, cycle=None):
+    import torch
+    from jr import synth
+    from jr.inception import build_inception_v3
+    from jr.init import init_params, unflatten
+    from oracle.inception_ref import InceptionV3Ref
+    torch.set_num_threads(os.cpu_count() or 8)
+    g = build_inception_v3(res, res)
+    ref = InceptionV3Ref(unflatten(g, init_params(g, seed)), torch.float64)
+    pool = cycle or batch
+    imgs = synth.fundus_batch(0, pool, res)
+    labels = synth.labels(0, pool)
+    state, losses = {}, []
+    out = {}
+    for step in range(steps):
+        k = (step * batch) % pool
+        x = imgs[k:k + batch].astype(np.float32) * np.float32(1 / 255)
+        y = labels[k:k + batch]
+        loss, probs, grads = ref.train_step(x, y, state)
+        losses.append(loss)
+        if step == 0:
+            out["logits"] = ref.last_logits
+            out["probs"] = probs
+            out["loss0"] = np.array(loss)
+            names = sorted(grads)
+            out["grad_names"] = np.array(names)
+            out["grad_norms"] = np.array([np.linalg.norm(grads[k_]) for k_ in names])
+    out["losses"] = np.array(losses)
+    out.update(res=np.array(res), batch=np.array(batch), seed=np.array(seed), pool=np.array(pool))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="ops,metrics,net107,net299,curve")
+    a = ap.parse_args()
+    os.makedirs(OUT, exist_ok=True)
+    todo = a.only.split(",")
+    t0 = time.time()
+    if "ops" in todo:
+        ops()
+    if "metrics" in todo:
+        metrics()
+    if "net107" in todo:
+        np.savez_compressed(os.path.join(OUT, "net_res107_b3.npz"), **_net(107, 3, 1))
+    if "net299" in todo:
+        np.savez_compressed(os.path.join(OUT, "net_res299_b4.npz"), **_net(299, 4, 0))
+    if "curve" in todo:
+        # 100 Nesterov steps at B=4, 299^2, fixed unshuffled stream of 8 images
+        np.savez_compressed(os.path.join(OUT, "loss_curve_res299_b4.npz"), **_net(299, 4, 0, steps=100, cycle=8))
+    print(f"golden fixtures written to {OUT} in {time.time() - t0:.0f}s")
+
+
+if __name__ == "__main__":
+    main()
