@@ -132,6 +132,15 @@ __device__ __forceinline__ void dma16(const float* src, float* lds_chunk) {
 
 // DBG (diagnostic builds only, jr_conv2d_debug_time): 1 = no MFMA,
 // 2 = no DMA after the first tile (results are wrong in both).
+//
+// Address generation.  When the reduction channel count (c_in for FWD,
+// c_out for DGRAD) is a multiple of BK, a K-tile never straddles a tap, so
+// the tap (r, c, channel base) is WAVE-UNIFORM: it lives in SGPRs, and each
+// DMA slot keeps a 64-bit base pointer fixed for the whole K loop; per tile
+// a lane only adds a scalar offset and checks its row's bounds.  Otherwise
+// (conv1, c_in = 3 padded to 4) every lane keeps its own mixed-radix k
+// counter (generic path).  WGRAD's A operand walks pixels along k, so its
+// lanes advance (b, oh, ow) counters.
 template <int OP, int BM, int BN, int WGM, int BK, int NBUF, int DBG = 0>
 __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int WGN = 4 / WGM;
@@ -162,15 +171,17 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   const int kt0 = blockIdx.z * g.kt_per_split;
   const int kt1 = min(g.ktiles, kt0 + g.kt_per_split);
   const float* zp = g_zero_page;
+  const int cred = OP == OP_FWD ? g.cp : g.cout;       // channel radix of the KC k index
+  const bool ut = (OP != OP_WGRAD) && (cred % BK == 0);  // wave-uniform tap (kernel arg)
 
   // ---------------------------------------------------------------- A state
-  // KC: instr j covers rows j*RPI.. ; lane -> (row, logical quad q)
-  // MC: instr j covers floats [256j, 256j+256) of [BK][BM]: lane -> (krow, col)
+  const float* a_ptr[A_PW];                 // per-slot base pointer (ut paths)
   int a_p0[A_PW], a_p1[A_PW], a_p2[A_PW];   // per-slot geometry fixed over K
-  int a_s0[A_PW], a_s1[A_PW], a_s2[A_PW];   // per-slot state advanced per K-tile
+  int a_s0[A_PW], a_s1[A_PW], a_s2[A_PW];   // per-lane k counters (generic / WGRAD)
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     const int j = wave + 4 * i;
+    a_ptr[i] = zp;
     a_p0[i] = a_p1[i] = a_p2[i] = 0;
     a_s0[i] = a_s1[i] = a_s2[i] = 0;
     if (j >= A_INSTR) continue;
@@ -180,6 +191,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       const int m = m0 + row;
       const int k = kt0 * BK + q * 4;
       if constexpr (OP == OP_FWD) {
+        int pix = 0;
         if (m < g.M) {
           const int hw = g.ho * g.wo;
           const int b = m / hw, rem = m - b * hw;
@@ -187,14 +199,17 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
           a_p0[i] = oh * g.sh - g.ph;
           a_p1[i] = ow * g.sw - g.pw;
           a_p2[i] = b * g.h * g.w;
+          pix = a_p2[i] + a_p0[i] * g.w + a_p1[i];
         } else {
           a_p0[i] = -(1 << 28);
         }
+        a_ptr[i] = g.A + ((long long)pix * g.xs + g.xo + q * 4);
         const int rc = k / g.cp;
         a_s2[i] = k - rc * g.cp;          // ci
         a_s0[i] = rc / g.kw;              // r
         a_s1[i] = rc - a_s0[i] * g.kw;    // c
       } else {  // DGRAD: m = (b,u,v) of the phase, k = (a, bb, co)
+        int pix = 0;
         if (m < g.M) {
           const int hw = g.hc * g.wc;
           const int b = m / hw, rem = m - b * hw;
@@ -202,9 +217,11 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
           a_p0[i] = u + g.ey;
           a_p1[i] = v + g.ex;
           a_p2[i] = b * g.ho * g.wo;
+          pix = a_p2[i] + a_p0[i] * g.wo + a_p1[i];
         } else {
           a_p0[i] = -(1 << 28);
         }
+        a_ptr[i] = g.A + ((long long)pix * g.ys + g.yo + q * 4);
         const int ab = k / g.cout;
         a_s2[i] = k - ab * g.cout;        // co
         a_s0[i] = ab / g.nb;              // a
@@ -232,10 +249,12 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     }
   }
   // ---------------------------------------------------------------- B state
+  const float* b_ptr[B_PW];
   int b_p0[B_PW], b_s0[B_PW], b_s1[B_PW], b_s2[B_PW];
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
     const int j = wave + 4 * i;
+    b_ptr[i] = zp;
     b_p0[i] = b_s0[i] = b_s1[i] = b_s2[i] = 0;
     if (j >= B_INSTR) continue;
     if constexpr (B_KC) {  // DGRAD: rows = ci, k = (a, bb, co)
@@ -243,6 +262,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       const int q = (lane % QPR) ^ ((row / SWZ) % QPR);
       const int nn = n0 + row;
       b_p0[i] = nn < g.N ? nn : -1;
+      b_ptr[i] = g.B + ((long long)(nn < g.N ? nn : 0) * g.cout + q * 4);
       const int k = kt0 * BK + q * 4;
       const int ab = k / g.cout;
       b_s2[i] = k - ab * g.cout;
@@ -252,76 +272,122 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       const int flat = j * 256 + lane * 4;
       const int krow = flat / BN, col = flat - krow * BN;
       b_p0[i] = (n0 + col < g.N) ? n0 + col : -1;
-      b_s0[i] = kt0 * BK + krow;          // k
+      b_s0[i] = kt0 * BK + krow;          // k of this lane at tile kt0
+      if constexpr (OP == OP_FWD)
+        b_ptr[i] = g.B + ((long long)b_s0[i] * g.N + (n0 + col));
+      else
+        b_ptr[i] = g.B + ((long long)b_s0[i] * g.ys + g.yo + n0 + col);
     }
   }
+  // wave-uniform tap counters of the ut paths, at tile kt0
+  int t_r = 0, t_c = 0, t_ch = 0;
+  if (ut) {
+    const int k = kt0 * BK;
+    const int rc = k / cred;
+    t_ch = k - rc * cred;
+    t_r = rc / (OP == OP_FWD ? g.kw : g.nb);
+    t_c = rc - t_r * (OP == OP_FWD ? g.kw : g.nb);
+  }
 
-  // Branch-free address generation: every operand slot keeps its k-position
-  // as a mixed-radix counter advanced by BK per tile (one conditional carry
-  // when the inner radix >= BK, the common case; a uniform slow path
-  // otherwise), and out-of-range taps select the zero page.
-  const bool a_multi = A_KC ? ((OP == OP_FWD ? g.cp : g.cout) < BK) : (g.wo < BK);
+  const bool a_multi = A_KC ? (cred < BK) : (g.wo < BK);
   const bool b_multi = B_KC ? (g.cout < BK) : false;
   auto issue = [&](int kt, float* __restrict__ As, float* __restrict__ Bs) {
-    (void)kt;
     // -------------------------------------------------------------- A
-#pragma unroll
-    for (int i = 0; i < A_PW; ++i) {
-      const int j = wave + 4 * i;
-      if (j >= A_INSTR) continue;
-      const float* src;
+    if (A_KC && ut) {
+      long long off;                          // wave-uniform element offset of the tap
+      int dr, dc;
       if constexpr (OP == OP_FWD) {
-        const int hi = a_p0[i] + a_s0[i], wi = a_p1[i] + a_s1[i];
-        const bool ok = (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w && a_s0[i] < g.kh;
-        const float* p = g.A + ((a_p2[i] + hi * g.w + wi) * g.xs + g.xo + a_s2[i]);
-        src = ok ? p : zp;
-        adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cp, g.kw, a_multi);
-      } else if constexpr (OP == OP_DGRAD) {
-        const int oh = a_p0[i] - a_s0[i], ow = a_p1[i] - a_s1[i];
-        const bool ok = (unsigned)oh < (unsigned)g.ho && (unsigned)ow < (unsigned)g.wo && a_s0[i] < g.na;
-        const float* p = g.A + ((a_p2[i] + oh * g.wo + ow) * g.ys + g.yo + a_s2[i]);
-        src = ok ? p : zp;
-        adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cout, g.nb, a_multi);
-      } else {  // WGRAD
-        const int hi = a_s1[i] * g.sh + a_p0[i], wi = a_s2[i] * g.sw + a_p1[i];
-        const bool ok = a_s0[i] < g.n && (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w;
-        const float* p = g.A + (((a_s0[i] * g.h + hi) * g.w + wi) * g.xs + g.xo + a_p2[i]);
-        src = ok ? p : zp;
-        adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.wo, g.ho, a_multi);
+        off = (long long)(t_r * g.w + t_c) * g.xs + t_ch;
+        dr = t_r; dc = t_c;
+      } else {
+        off = -(long long)(t_r * g.wo + t_c) * g.ys + t_ch;
+        dr = -t_r; dc = -t_c;
       }
-      dma16(src, As + j * 256);
+      const int hmax = OP == OP_FWD ? g.h : g.ho, wmax = OP == OP_FWD ? g.w : g.wo;
+#pragma unroll
+      for (int i = 0; i < A_PW; ++i) {
+        const int j = wave + 4 * i;
+        if (j >= A_INSTR) continue;
+        const bool ok = (unsigned)(a_p0[i] + dr) < (unsigned)hmax && (unsigned)(a_p1[i] + dc) < (unsigned)wmax;
+        dma16(ok ? a_ptr[i] + off : zp, As + j * 256);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_PW; ++i) {
+        const int j = wave + 4 * i;
+        if (j >= A_INSTR) continue;
+        const float* src = zp;
+        if constexpr (OP == OP_FWD) {
+          const int hi = a_p0[i] + a_s0[i], wi = a_p1[i] + a_s1[i];
+          const bool ok = (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w && a_s0[i] < g.kh;
+          const float* p = g.A + ((a_p2[i] + hi * g.w + wi) * g.xs + g.xo + a_s2[i]);
+          src = ok ? p : zp;
+          adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cp, g.kw, a_multi);
+        } else if constexpr (OP == OP_DGRAD) {
+          const int oh = a_p0[i] - a_s0[i], ow = a_p1[i] - a_s1[i];
+          const bool ok = (unsigned)oh < (unsigned)g.ho && (unsigned)ow < (unsigned)g.wo && a_s0[i] < g.na;
+          const float* p = g.A + ((a_p2[i] + oh * g.wo + ow) * g.ys + g.yo + a_s2[i]);
+          src = ok ? p : zp;
+          adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cout, g.nb, a_multi);
+        } else {  // WGRAD
+          const int hi = a_s1[i] * g.sh + a_p0[i], wi = a_s2[i] * g.sw + a_p1[i];
+          const bool ok = a_s0[i] < g.n && (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w;
+          const float* p = g.A + (((a_s0[i] * g.h + hi) * g.w + wi) * g.xs + g.xo + a_p2[i]);
+          src = ok ? p : zp;
+          adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.wo, g.ho, a_multi);
+        }
+        dma16(src, As + j * 256);
+      }
     }
     // -------------------------------------------------------------- B
+    if constexpr (B_KC) {  // DGRAD: W[(r0+sh*a, c0+sw*bb)][ci][co]
+      if (ut) {
+        const long long off = (long long)((g.r0 + g.sh * t_r) * g.kw + (g.c0 + g.sw * t_c)) * g.cin * g.cout + t_ch;
 #pragma unroll
-    for (int i = 0; i < B_PW; ++i) {
-      const int j = wave + 4 * i;
-      if (j >= B_INSTR) continue;
-      const float* src;
-      if constexpr (B_KC) {  // DGRAD: W[(r0+sh*a, c0+sw*bb)][ci][co]
-        const bool ok = b_p0[i] >= 0 && b_s0[i] < g.na;
-        const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
-        const float* p = g.B + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
-        src = ok ? p : zp;
-        adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
+        for (int i = 0; i < B_PW; ++i) {
+          const int j = wave + 4 * i;
+          if (j >= B_INSTR) continue;
+          dma16(b_p0[i] >= 0 ? b_ptr[i] + off : zp, Bs + j * 256);
+        }
       } else {
-        const int k = b_s0[i];
+#pragma unroll
+        for (int i = 0; i < B_PW; ++i) {
+          const int j = wave + 4 * i;
+          if (j >= B_INSTR) continue;
+          const bool ok = b_p0[i] >= 0 && b_s0[i] < g.na;
+          const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
+          const float* p = g.B + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
+          dma16(ok ? p : zp, Bs + j * 256);
+          adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
+        }
+      }
+    } else {
+      const int kbase = kt * BK;                                   // wave-uniform
+      const long long off = (long long)(kbase - kt0 * BK) * (OP == OP_FWD ? g.N : g.ys);
+#pragma unroll
+      for (int i = 0; i < B_PW; ++i) {
+        const int j = wave + 4 * i;
+        if (j >= B_INSTR) continue;
+        const int k = b_s0[i] + (kbase - kt0 * BK);
         bool ok = b_p0[i] >= 0 && k < g.K;
-        const float* p;
+        const float* p = b_ptr[i] + off;
         if constexpr (OP == OP_FWD) {
-          int row = k;
           if (g.cp != g.cin) {  // virtual channel padding (c_in % 4 != 0): uniform branch
             const int rc = k / g.cp, ci = k - rc * g.cp;
             ok = ok && ci < g.cin;
-            row = rc * g.cin + ci;
+            p = g.B + ((rc * g.cin + ci) * g.N + b_p0[i]);
           }
-          p = g.B + (row * g.N + b_p0[i]);
-        } else {  // WGRAD: dy rows
-          p = g.B + (k * g.ys + g.yo + b_p0[i]);
         }
-        src = ok ? p : zp;
-        b_s0[i] += BK;
+        dma16(ok ? p : zp, Bs + j * 256);
       }
-      dma16(src, Bs + j * 256);
+    }
+    // advance the wave-uniform tap by BK
+    if (ut) {
+      t_ch += BK;
+      if (t_ch == cred) {
+        t_ch = 0;
+        if (++t_c == (OP == OP_FWD ? g.kw : g.nb)) { t_c = 0; ++t_r; }
+      }
     }
   };
 
@@ -363,41 +429,40 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       // still in flight (without them it drains every DMA first).
       auto stage = [&](const float* __restrict__ As, const float* __restrict__ Bs, float* __restrict__ wA,
                        float* __restrict__ wB) {
-      // 1) all of this lane's operand fragments of tile kt: LDS -> VGPRs,
-      //    before this iteration's DMA is issued.
+        // 1) this lane's operand fragments of tile kt: LDS -> VGPRs
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        if constexpr (A_KC) {
-          const int row = wm0 + i * 32 + l31;
-          const int f = (row / SWZ) % QPR;
+        for (int i = 0; i < TM; ++i) {
+          if constexpr (A_KC) {
+            const int row = wm0 + i * 32 + l31;
+            const int f = (row / SWZ) % QPR;
 #pragma unroll
-          for (int t = 0; t < QPR / 2; ++t) {
-            const float4 v = *reinterpret_cast<const float4*>(As + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
-            af[i][4 * t + 0] = v.x; af[i][4 * t + 1] = v.y; af[i][4 * t + 2] = v.z; af[i][4 * t + 3] = v.w;
+            for (int t = 0; t < QPR / 2; ++t) {
+              const float4 v = *reinterpret_cast<const float4*>(As + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
+              af[i][4 * t + 0] = v.x; af[i][4 * t + 1] = v.y; af[i][4 * t + 2] = v.z; af[i][4 * t + 3] = v.w;
+            }
+          } else {
+#pragma unroll
+            for (int s = 0; s < HALF; ++s) af[i][s] = As[(lh * HALF + s) * BM + wm0 + i * 32 + l31];
           }
-        } else {
-#pragma unroll
-          for (int s = 0; s < HALF; ++s) af[i][s] = As[(lh * HALF + s) * BM + wm0 + i * 32 + l31];
         }
-      }
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if constexpr (B_KC) {
-          const int row = wn0 + j * 32 + l31;
-          const int f = (row / SWZ) % QPR;
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (B_KC) {
+            const int row = wn0 + j * 32 + l31;
+            const int f = (row / SWZ) % QPR;
 #pragma unroll
-          for (int t = 0; t < QPR / 2; ++t) {
-            const float4 v = *reinterpret_cast<const float4*>(Bs + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
-            bfr[j][4 * t + 0] = v.x; bfr[j][4 * t + 1] = v.y; bfr[j][4 * t + 2] = v.z; bfr[j][4 * t + 3] = v.w;
+            for (int t = 0; t < QPR / 2; ++t) {
+              const float4 v = *reinterpret_cast<const float4*>(Bs + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
+              bfr[j][4 * t + 0] = v.x; bfr[j][4 * t + 1] = v.y; bfr[j][4 * t + 2] = v.z; bfr[j][4 * t + 3] = v.w;
+            }
+          } else {
+#pragma unroll
+            for (int s = 0; s < HALF; ++s) bfr[j][s] = Bs[(lh * HALF + s) * BN + wn0 + j * 32 + l31];
           }
-        } else {
-#pragma unroll
-          for (int s = 0; s < HALF; ++s) bfr[j][s] = Bs[(lh * HALF + s) * BN + wn0 + j * 32 + l31];
         }
-      }
-      // 2) DMA of tile kt+NBUF-1 into the buffer read in iteration kt-1
-      //    (released by the barrier that ended it)
-      if (DBG != 2 && kt + NBUF - 1 < kt1) issue(kt + NBUF - 1, wA, wB);
+        // 2) DMA of tile kt+NBUF-1 into the buffer read in iteration kt-1
+        //    (released by the barrier that ended it)
+        if (DBG != 2 && kt + NBUF - 1 < kt1) issue(kt + NBUF - 1, wA, wB);
       };
       stage(smem + cur * (ASZ + BSZ), smem + cur * (ASZ + BSZ) + ASZ, smem + nxt * (ASZ + BSZ),
             smem + nxt * (ASZ + BSZ) + ASZ);
