@@ -40,3 +40,21 @@ for (n, op), (r, t, t2) in zip(seq, last):
 for t, s in sorted(out, reverse=True)[:int(sys.argv[3]) if len(sys.argv) > 3 else 40]:
     print(s)
 print(f"total conv {tot_t/1e6:.2f} ms, {tot_f/tot_t/1e3:.1f} TF/s")
+
+# ---- whole-step breakdown: kernels between the last two optimizer launches
+opt = [i for i, r in enumerate(rows) if "k_nesterov" in r["Kernel_Name"] or "k_sgd" in r["Kernel_Name"]]
+if len(opt) >= 2:
+    a, b = opt[-2] + 1, opt[-1] + 1
+    step = rows[a:b]
+    t0 = int(step[0]["Start_Timestamp"]); t1 = int(step[-1]["End_Timestamp"])
+    from collections import defaultdict
+    cat = defaultdict(float)
+    for r in step:
+        n = r["Kernel_Name"]
+        key = n.split("(")[0].replace("void ", "")
+        key = key.split("<")[0]
+        cat[key] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    busy = sum(cat.values())
+    print(f"\nlast step: wall {(t1 - t0)/1e6:.2f} ms, kernel-busy {busy:.2f} ms, {len(step)} kernels")
+    for k, v in sorted(cat.items(), key=lambda kv: -kv[1]):
+        print(f"  {v:8.3f} ms  {k}")
