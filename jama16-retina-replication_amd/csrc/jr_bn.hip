@@ -139,30 +139,34 @@ __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, cons
   }
 }
 
-// Fixed-order combine of the chunk partials: block = 16 channels x 16 chunk
-// lanes; lane ty sums chunks ty, ty+16, ... then lane sums are added in lane
-// order (deterministic, independent of timing).
+// Fixed-order combine of the chunk partials: one wave per channel; lane j
+// sums chunks j, j+64, ... (four loads in flight), then a fixed xor-butterfly
+// adds the 64 lane sums (deterministic, independent of timing).
 // MODE 0: mean, invstd.   MODE 1: k1 = sum dy'/m, k2 = sum dy'xhat/m, dbeta.
 template <int MODE>
 __global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ part, int nchunks, int c,
                                                      int64_t m, float eps, float* out0, float* out1,
                                                      float* dbeta) {
-  __shared__ double red[2][16][17];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int k = blockIdx.x * 16 + tx;
-  double s0 = 0, s1 = 0;
-  if (k < c) {
-    for (int i = ty; i < nchunks; i += 16) {
-      s0 += part[(int64_t)i * 2 * c + k];
-      s1 += part[(int64_t)i * 2 * c + c + k];
-    }
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= c) return;   // wave-uniform
+  const double* p0 = part + k;
+  const double* p1 = part + c + k;
+  const int64_t st = 2 * (int64_t)c;
+  double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+  int i = lane;
+  for (; i + 64 < nchunks; i += 128) {
+    const double x0 = p0[i * st], y0 = p1[i * st], x1 = p0[(i + 64) * st], y1 = p1[(i + 64) * st];
+    a0 += x0; b0 += y0; a1 += x1; b1 += y1;
   }
-  red[0][ty][tx] = s0;
-  red[1][ty][tx] = s1;
-  __syncthreads();
-  if (ty != 0 || k >= c) return;
-  s0 = 0; s1 = 0;
-  for (int j = 0; j < 16; ++j) { s0 += red[0][j][tx]; s1 += red[1][j][tx]; }
+  if (i < nchunks) { a0 += p0[i * st]; b0 += p1[i * st]; }
+  double s0 = a0 + a1, s1 = b0 + b1;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o, 64);
+    s1 += __shfl_xor(s1, o, 64);
+  }
+  if (lane != 0) return;
   const double inv_m = 1.0 / (double)m;
   if (MODE == 0) {
     const double mu = s0 * inv_m;
@@ -279,7 +283,7 @@ JR_API int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps
                        part);
   rc = check_launch("bn_stats reduce");
   if (rc) return rc;
-  hipLaunchKernelGGL((k_bn_finalize<0>), dim3((int)ceil_div(c, 16)), dim3(256), 0, s, part, g.nchunks, c, m,
+  hipLaunchKernelGGL((k_bn_finalize<0>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, g.nchunks, c, m,
                      eps, mean, invstd, (float*)nullptr);
   return check_launch("bn_stats finalize");
 }
@@ -328,7 +332,7 @@ JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t d
                        beta, part);
   rc = check_launch("bn_bwd reduce");
   if (rc) return rc;
-  hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 16)), dim3(256), 0, s, part, g.nchunks, c, m,
+  hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, g.nchunks, c, m,
                      0.f, k1, k2, dbeta);
   rc = check_launch("bn_bwd finalize");
   if (rc) return rc;

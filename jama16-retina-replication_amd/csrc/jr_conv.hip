@@ -511,19 +511,61 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   }
 }
 
-// out[out_row(m) + n] (+)= sum_z slab[z][m][n]   (fixed order)
+// out[out_row(m) + n] (+)= sum_z slab[z][m][n], float4 along n (N % 16 == 0
+// and channel offsets/strides % 4 == 0 keep every access 16-byte aligned).
+// Block = G z-lanes x (256 / G) float4 columns: z-lane zg sums slabs zg,
+// zg + G, ... and the G lane sums are added in zg order through LDS, so the
+// result depends only on (M, N, splits), never on timing.  G grows when
+// M*N is small and splits large (the wgrad case: a few thousand outputs, up
+// to 256 slabs) so the reduce still spreads over the whole chip.
 template <int OP>
-__global__ void k_splitk_reduce(const float* __restrict__ slab, int splits, ConvArgs g, float* out) {
-  const long long total = (long long)g.M * g.N;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int m = (int)(e / g.N), n = (int)(e - (long long)m * g.N);
+__global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ slab, int splits, int G,
+                                                       ConvArgs g, float* out) {
+  __shared__ float4 part[256];
+  const int cols = 256 / G;
+  const int t = threadIdx.x;
+  const int zg = t / cols, cl = t - zg * cols;
+  const int n4 = g.N >> 2;
+  const long long total = (long long)g.M * n4;
+  const long long zs = g.slab_elems >> 2;
+  for (long long e0 = (long long)blockIdx.x * cols; e0 < total; e0 += (long long)gridDim.x * cols) {
+    const long long e = e0 + cl;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < total) {
+      const float4* src = reinterpret_cast<const float4*>(slab) + e;
+      int z = zg;
+      for (; z + 3 * G < splits; z += 4 * G) {
+        const float4 a = src[z * zs], b = src[(z + G) * zs], c = src[(z + 2 * G) * zs], d = src[(z + 3 * G) * zs];
+        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+        s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+        s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
+        s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
+      }
+      for (; z < splits; z += G) {
+        const float4 a = src[z * zs];
+        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+      }
+    }
+    if (G > 1) {
+      part[t] = s;
+      __syncthreads();
+      if (zg == 0) {
+        for (int k = 1; k < G; ++k) {
+          const float4 a = part[k * cols + cl];
+          s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+        }
+      }
+      __syncthreads();
+    }
+    if (zg != 0 || e >= total) continue;
+    const int m = (int)(e / n4), q = (int)(e - (long long)m * n4);
     const long long base = out_row<OP>(g, m);
     if (base < 0) continue;
-    float s = slab[e];
-    for (int z = 1; z < splits; ++z) s += slab[z * g.slab_elems + e];
-    float* p = out + base + n;
-    if (g.accumulate) s += *p;
+    float4* p = reinterpret_cast<float4*>(out + base + q * 4);
+    if (g.accumulate) {
+      const float4 o = *p;
+      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+    }
     *p = s;
   }
 }
@@ -549,6 +591,9 @@ static constexpr TileCfg kCfgs[] = {
     {128, 32, 4, 32, 3, 0.75},   // 8: wave 32x32, 60 KiB
     {64, 128, 2, 32, 2, 0.80},   // 9: wave 32x64, 48 KiB
     {128, 64, 2, 16, 2, 0.90},   // 10: wave 64x32, 24 KiB
+    {128, 192, 2, 16, 3, 1.02},  // 11: wave 64x96, 60 KiB (N = 192 layers)
+    {256, 96, 4, 16, 3, 1.02},   // 12: wave 64x96, 66 KiB (N = 96 layers)
+    {256, 128, 2, 16, 3, 1.04},  // 13: wave 128x64, 72 KiB
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -556,8 +601,15 @@ struct Phase {
   int py, px, r0, c0, na, nb, ey, ex, hc, wc;
 };
 
+// A config id is tile | (splits << 8): splits == 0 lets the planner pick
+// the split-K factor, otherwise it is forced (autotuning explores both).
+constexpr int kSplitShift = 8;
+static int cfg_tile(int cfg) { return cfg & ((1 << kSplitShift) - 1); }
+static int cfg_splits(int cfg) { return cfg >> kSplitShift; }
+
 struct Plan {
-  int cfg;
+  int cfg;   // encoded id
+  int tile;
   int M, N, K;
   int mt, nt, ktiles, splits, kt_per_split;
 };
@@ -586,8 +638,8 @@ static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
 
 static Plan plan_with(int cfg, int M, int N, int K) {
   Plan p{};
-  p.M = M; p.N = N; p.K = K; p.cfg = cfg;
-  const TileCfg& t = kCfgs[cfg];
+  p.M = M; p.N = N; p.K = K; p.cfg = cfg; p.tile = cfg_tile(cfg);
+  const TileCfg& t = kCfgs[p.tile];
   p.mt = (int)ceil_div(M, t.bm);
   p.nt = (int)ceil_div(N, t.bn);
   p.ktiles = (int)ceil_div(K, t.bk);
@@ -599,6 +651,7 @@ static Plan plan_with(int cfg, int M, int N, int K) {
     const int max_by_k = std::max(1, p.ktiles / 8);
     splits = std::min(std::min(splits, max_by_k), 256);
   }
+  if (cfg_splits(cfg) > 0) splits = std::min(cfg_splits(cfg), std::max(p.ktiles, 1));
   p.kt_per_split = (int)ceil_div(std::max(p.ktiles, 1), splits);
   p.splits = (int)ceil_div(std::max(p.ktiles, 1), p.kt_per_split);
   return p;
@@ -661,7 +714,10 @@ static void launch_op(int cfg, const ConvArgs& a, dim3 grid, hipStream_t s) {
     case 7: launch_cfg<OP, 7>(a, grid, s); break;
     case 8: launch_cfg<OP, 8>(a, grid, s); break;
     case 9: launch_cfg<OP, 9>(a, grid, s); break;
-    default: launch_cfg<OP, 10>(a, grid, s); break;
+    case 10: launch_cfg<OP, 10>(a, grid, s); break;
+    case 11: launch_cfg<OP, 11>(a, grid, s); break;
+    case 12: launch_cfg<OP, 12>(a, grid, s); break;
+    default: launch_cfg<OP, 13>(a, grid, s); break;
   }
 }
 
@@ -720,12 +776,15 @@ static int run_gemm(ConvArgs a, const Plan& p, float* out, void* ws, size_t ws_b
     a.C = out;
   }
   dim3 grid(p.mt * p.nt, 1, p.splits);
-  launch_op<OP>(p.cfg, a, grid, s);
+  launch_op<OP>(p.tile, a, grid, s);
   int rc = check_launch("conv gemm");
   if (rc || p.splits <= 1) return rc;
-  const long long total = (long long)p.M * p.N;
-  const int blocks = (int)std::min<long long>(ceil_div(total, 256), 4096);
-  hipLaunchKernelGGL((k_splitk_reduce<OP>), dim3(blocks), dim3(256), 0, s, (const float*)ws, p.splits, a, out);
+  const long long total = (long long)p.M * p.N / 4;   // float4 columns
+  int G = 1;                                            // z-lanes per column
+  while (G < 64 && G * 4 <= p.splits && total * G < 128 * 1024) G *= 2;
+  const long long cols = 256 / G;
+  const int blocks = (int)std::min<long long>(ceil_div(total, cols), 8192);
+  hipLaunchKernelGGL((k_splitk_reduce<OP>), dim3(blocks), dim3(256), 0, s, (const float*)ws, p.splits, G, a, out);
   return check_launch("conv split-k reduce");
 }
 
@@ -742,7 +801,8 @@ static Plan plan_for(const jr_conv_desc* d, int op, const Phase* ph, int force_c
   return make_plan(op, M, N, K, d, force_cfg);
 }
 
-// Workspace: the max over every candidate config, so any tuned choice fits.
+// Workspace: twice the max over every candidate tile's planned split-K, so
+// any tuned choice fits.
 static size_t ws_bytes_for(const jr_conv_desc* d, int op) {
   Phase ph[64];
   int nph = 1;
@@ -753,7 +813,7 @@ static size_t ws_bytes_for(const jr_conv_desc* d, int op) {
     for (int c = 0; c < kNumCfgs; ++c)
       w = std::max(w, plan_ws(plan_for(d, op, op == OP_DGRAD ? &ph[i] : nullptr, c)));
   }
-  return w;
+  return 2 * w;   // room for the autotuner's doubled split-K factors
 }
 
 // Runs the op; force_cfg >= 0 overrides the plan (autotuning).
@@ -823,21 +883,41 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
     if (op == OP_DGRAD && (ph[i].na == 0 || ph[i].nb == 0 || ph[i].hc == 0 || ph[i].wc == 0)) continue;
     int M, N, K;
     gemm_dims(d, op, op == OP_DGRAD ? &ph[i] : nullptr, &M, &N, &K);
-    float best_t = 1e30f;
     int best_c = heuristic_cfg(M, N, K);
-    for (int c = 0; c < kNumCfgs; ++c) {
-      if (plan_ws(plan_with(c, M, N, K)) > ws_bytes) continue;
+    float best_t = 1e30f;
+    auto time_cfg = [&](int c) -> float {
+      if (plan_ws(plan_with(c, M, N, K)) > ws_bytes) return 1e30f;
       rc = run_conv(d, op, dtype, A, B, C, 0, ws, ws_bytes, stream, c, op == OP_DGRAD ? i : -1);  // warm-up
-      if (rc) break;
+      if (rc) return 1e30f;
       (void)hipEventRecord(e0, s);
-      for (int r = 0; r < reps; ++r)
+      for (int r = 0; r < reps && !rc; ++r)
         rc = run_conv(d, op, dtype, A, B, C, 0, ws, ws_bytes, stream, c, op == OP_DGRAD ? i : -1);
       (void)hipEventRecord(e1, s);
-      if (rc) break;
-      if (hipEventSynchronize(e1) != hipSuccess) { rc = fail(JR_ERR_HIP, "autotune: event sync failed"); break; }
+      if (rc) return 1e30f;
+      if (hipEventSynchronize(e1) != hipSuccess) { rc = fail(JR_ERR_HIP, "autotune: event sync failed"); return 1e30f; }
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, e0, e1);
       if (ms < best_t) { best_t = ms; best_c = c; }
+      return ms;
+    };
+    // pass 1: every tile with the planner's split-K factor
+    float tile_t[kNumCfgs];
+    for (int c = 0; c < kNumCfgs && !rc; ++c) tile_t[c] = time_cfg(c);
+    // pass 2: the three fastest tiles with other split-K factors
+    for (int pick = 0; pick < 3 && !rc; ++pick) {
+      int c = -1;
+      for (int k = 0; k < kNumCfgs; ++k)
+        if (tile_t[k] < 1e29f && (c < 0 || tile_t[k] < tile_t[c])) c = k;
+      if (c < 0) break;
+      tile_t[c] = 1e30f;
+      const Plan dp = plan_with(c, M, N, K);
+      int prev = -1;
+      for (int v : {1, dp.splits / 4, dp.splits / 2, dp.splits * 2}) {
+        if (v < 1 || v == dp.splits || v == prev || v > 256 || v > dp.ktiles) continue;
+        prev = v;
+        time_cfg(c | (v << kSplitShift));
+        if (rc) break;
+      }
     }
     if (rc) break;
     std::lock_guard<std::mutex> lk(g_tune_mu);
@@ -921,7 +1001,8 @@ JR_API int jr_conv2d_debug_time(const jr_conv_desc* d, int cfg, int dbg, const v
 JR_API int jr_conv2d_set_config(const jr_conv_desc* d, int op, int phase, int cfg) {
   int rc = validate(d, op);
   if (rc) return rc;
-  if (cfg < 0 || cfg >= kNumCfgs) return fail(JR_ERR_INVALID, "conv set_config: bad config index");
+  if (cfg < 0 || cfg_tile(cfg) >= kNumCfgs || cfg_splits(cfg) > 256)
+    return fail(JR_ERR_INVALID, "conv set_config: bad config index");
   Phase ph[64];
   int nph = 1;
   if (op == OP_DGRAD) {

@@ -124,7 +124,8 @@ def test_conv_fwd_dgrad_wgrad(case):
 @pytest.mark.parametrize("case", [(2, 17, 17, 64, 96, 3, 3, 1, "same"), (2, 17, 17, 48, 64, 3, 3, 2, "valid"),
                                   (2, 11, 11, 3, 32, 3, 3, 2, "valid")])
 def test_conv_every_tile_config(case):
-    """Every tile configuration the autotuner may pick is correct."""
+    """Every tile configuration the autotuner may pick is correct, with the
+    planner's split-K factor and with forced factors (id = tile | splits << 8)."""
     ffi = _lib()
     L = ffi.load()
     n, h, w, cin, cout, kh, kw, s, pad = case
@@ -141,8 +142,10 @@ def test_conv_every_tile_config(case):
     ref_dw = R.conv2d_bwd_filter(x, dy, wt.shape, s, pad)
     X, W, DY = dev(xp), dev(wt), dev(dy)
     wsb = max(L.jr_conv2d_workspace_size(ctypes.byref(d), op, 0) for op in range(3))
+    wsb += 3 * 4 * max(n * ho * wo * cout, kh * kw * cs * cout, n * h * w * cs)   # forced splits of 3
     ws = torch.zeros(wsb // 4 + 4, device="cuda")
-    for cfg in range(L.jr_conv2d_num_configs()):
+    cfgs = [t | (sp << 8) for t in range(L.jr_conv2d_num_configs()) for sp in (0, 1, 3)]  # forced split-K
+    for cfg in cfgs:
         ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, 0, cfg))
         ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 2, 0, cfg))
         Y = torch.zeros(ref.size, device="cuda")

@@ -58,3 +58,9 @@ if len(opt) >= 2:
     print(f"\nlast step: wall {(t1 - t0)/1e6:.2f} ms, kernel-busy {busy:.2f} ms, {len(step)} kernels")
     for k, v in sorted(cat.items(), key=lambda kv: -kv[1]):
         print(f"  {v:8.3f} ms  {k}")
+
+# ---- split-K reduce launches of the last step, largest first
+red = sorted(((t2, s) for (t, s), (_, _, t2) in zip(out, last) if t2 > 0), reverse=True)
+print(f"\nsplit-K reduces: {len(red)} launches, {sum(t for t, _ in red)/1e6:.3f} ms")
+for t2, s in red[:int(sys.argv[4]) if len(sys.argv) > 4 else 10]:
+    print(f"  {t2/1e3:7.1f}us  {s[:60]}")
