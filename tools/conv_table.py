@@ -64,3 +64,20 @@ red = sorted(((t2, s) for (t, s), (_, _, t2) in zip(out, last) if t2 > 0), rever
 print(f"\nsplit-K reduces: {len(red)} launches, {sum(t for t, _ in red)/1e6:.3f} ms")
 for t2, s in red[:int(sys.argv[4]) if len(sys.argv) > 4 else 10]:
     print(f"  {t2/1e3:7.1f}us  {s[:60]}")
+
+# ---- rocprofv3-style stats restricted to the last complete steps (the
+# process-wide run_kernel_stats.csv also holds autotuning and warm-up calls)
+if len(sys.argv) > 5 and len(opt) >= 2:
+    nsteps = min(int(sys.argv[6]) if len(sys.argv) > 6 else 3, len(opt) - 1)
+    a, b = opt[-1 - nsteps] + 1, opt[-1] + 1
+    per = defaultdict(list)
+    for r in rows[a:b]:
+        per[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    tot = sum(sum(v) for v in per.values())
+    with open(sys.argv[5], "w", newline="") as f:
+        w = csv.writer(f, quoting=csv.QUOTE_NONNUMERIC)
+        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs", "CallsPerStep"])
+        for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+            w.writerow([k, len(v), sum(v), round(sum(v) / len(v), 1), round(100 * sum(v) / tot, 2), min(v), max(v),
+                        round(len(v) / nsteps, 2)])
+    print(f"\nwrote step-window stats over {nsteps} steps to {sys.argv[5]}")
