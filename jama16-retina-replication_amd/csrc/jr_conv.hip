@@ -36,6 +36,7 @@
 #include "jr_common.h"
 
 #include <array>
+#include <type_traits>
 #include <map>
 #include <mutex>
 
@@ -141,7 +142,7 @@ __device__ __forceinline__ void dma16(const float* src, float* lds_chunk) {
 // (conv1, c_in = 3 padded to 4) every lane keeps its own mixed-radix k
 // counter (generic path).  WGRAD's A operand walks pixels along k, so its
 // lanes advance (b, oh, ow) counters.
-template <int OP, int BM, int BN, int WGM, int BK, int NBUF, int DBG = 0>
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, int DBG = 0>
 __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int WGN = 4 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -172,7 +173,8 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   const int kt1 = min(g.ktiles, kt0 + g.kt_per_split);
   const float* zp = g_zero_page;
   const int cred = OP == OP_FWD ? g.cp : g.cout;       // channel radix of the KC k index
-  const bool ut = (OP != OP_WGRAD) && (cred % BK == 0);  // wave-uniform tap (kernel arg)
+  constexpr bool ut = UT;   // wave-uniform tap: host guarantees cred % BK == 0 (not WGRAD)
+  static_assert(!(UT && OP == OP_WGRAD), "WGRAD has no uniform-tap path");
 
   // ---------------------------------------------------------------- A state
   const float* a_ptr[A_PW];                 // per-slot base pointer (ut paths)
@@ -184,7 +186,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     a_ptr[i] = zp;
     a_p0[i] = a_p1[i] = a_p2[i] = 0;
     a_s0[i] = a_s1[i] = a_s2[i] = 0;
-    if (j >= A_INSTR) continue;
+    if (A_INSTR % 4 != 0 && j >= A_INSTR) continue;
     if constexpr (A_KC) {
       const int row = j * RPI + lane / QPR;
       const int q = (lane % QPR) ^ ((row / SWZ) % QPR);
@@ -256,7 +258,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     const int j = wave + 4 * i;
     b_ptr[i] = zp;
     b_p0[i] = b_s0[i] = b_s1[i] = b_s2[i] = 0;
-    if (j >= B_INSTR) continue;
+    if (B_INSTR % 4 != 0 && j >= B_INSTR) continue;
     if constexpr (B_KC) {  // DGRAD: rows = ci, k = (a, bb, co)
       const int row = j * RPI + lane / QPR;
       const int q = (lane % QPR) ^ ((row / SWZ) % QPR);
@@ -281,7 +283,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   }
   // wave-uniform tap counters of the ut paths, at tile kt0
   int t_r = 0, t_c = 0, t_ch = 0;
-  if (ut) {
+  if constexpr (ut) {
     const int k = kt0 * BK;
     const int rc = k / cred;
     t_ch = k - rc * cred;
@@ -293,7 +295,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   const bool b_multi = B_KC ? (g.cout < BK) : false;
   auto issue = [&](int kt, float* __restrict__ As, float* __restrict__ Bs) {
     // -------------------------------------------------------------- A
-    if (A_KC && ut) {
+    if constexpr (A_KC && ut) {
       long long off;                          // wave-uniform element offset of the tap
       int dr, dc;
       if constexpr (OP == OP_FWD) {
@@ -307,7 +309,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
 #pragma unroll
       for (int i = 0; i < A_PW; ++i) {
         const int j = wave + 4 * i;
-        if (j >= A_INSTR) continue;
+        if (A_INSTR % 4 != 0 && j >= A_INSTR) continue;
         const bool ok = (unsigned)(a_p0[i] + dr) < (unsigned)hmax && (unsigned)(a_p1[i] + dc) < (unsigned)wmax;
         dma16(ok ? a_ptr[i] + off : zp, As + j * 256);
       }
@@ -315,7 +317,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
 #pragma unroll
       for (int i = 0; i < A_PW; ++i) {
         const int j = wave + 4 * i;
-        if (j >= A_INSTR) continue;
+        if (A_INSTR % 4 != 0 && j >= A_INSTR) continue;
         const float* src = zp;
         if constexpr (OP == OP_FWD) {
           const int hi = a_p0[i] + a_s0[i], wi = a_p1[i] + a_s1[i];
@@ -341,19 +343,19 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     }
     // -------------------------------------------------------------- B
     if constexpr (B_KC) {  // DGRAD: W[(r0+sh*a, c0+sw*bb)][ci][co]
-      if (ut) {
+      if constexpr (ut) {
         const long long off = (long long)((g.r0 + g.sh * t_r) * g.kw + (g.c0 + g.sw * t_c)) * g.cin * g.cout + t_ch;
 #pragma unroll
         for (int i = 0; i < B_PW; ++i) {
           const int j = wave + 4 * i;
-          if (j >= B_INSTR) continue;
+          if (B_INSTR % 4 != 0 && j >= B_INSTR) continue;
           dma16(b_p0[i] >= 0 ? b_ptr[i] + off : zp, Bs + j * 256);
         }
       } else {
 #pragma unroll
         for (int i = 0; i < B_PW; ++i) {
           const int j = wave + 4 * i;
-          if (j >= B_INSTR) continue;
+          if (B_INSTR % 4 != 0 && j >= B_INSTR) continue;
           const bool ok = b_p0[i] >= 0 && b_s0[i] < g.na;
           const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
           const float* p = g.B + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
@@ -367,12 +369,12 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
 #pragma unroll
       for (int i = 0; i < B_PW; ++i) {
         const int j = wave + 4 * i;
-        if (j >= B_INSTR) continue;
+        if (B_INSTR % 4 != 0 && j >= B_INSTR) continue;
         const int k = b_s0[i] + (kbase - kt0 * BK);
         bool ok = b_p0[i] >= 0 && k < g.K;
         const float* p = b_ptr[i] + off;
         if constexpr (OP == OP_FWD) {
-          if (g.cp != g.cin) {  // virtual channel padding (c_in % 4 != 0): uniform branch
+          if (!ut && g.cp != g.cin) {  // virtual channel padding (c_in % 4 != 0): uniform branch
             const int rc = k / g.cp, ci = k - rc * g.cp;
             ok = ok && ci < g.cin;
             p = g.B + ((rc * g.cin + ci) * g.N + b_p0[i]);
@@ -382,12 +384,14 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       }
     }
     // advance the wave-uniform tap by BK
-    if (ut) {
+    if constexpr (ut) {   // branch-free (s_cselect) so the K loop stays one basic block
       t_ch += BK;
-      if (t_ch == cred) {
-        t_ch = 0;
-        if (++t_c == (OP == OP_FWD ? g.kw : g.nb)) { t_c = 0; ++t_r; }
-      }
+      const bool w1 = t_ch == cred;
+      t_ch = w1 ? 0 : t_ch;
+      t_c += w1 ? 1 : 0;
+      const bool w2 = t_c == (OP == OP_FWD ? g.kw : g.nb);
+      t_c = w2 ? 0 : t_c;
+      t_r += w2 ? 1 : 0;
     }
   };
 
@@ -412,6 +416,82 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     for (int i = 0; i < B_PW; ++i) per_tile += (wave + 4 * i < B_INSTR);
   }
 
+  // One K-tile: fragments of tile kt (LDS -> VGPRs), DMA of tile
+  // kt+NBUF-1 into the buffer read in iteration kt-1 (released by the
+  // barrier that ended it), MFMAs from registers.  The reads and the DMA go
+  // through __restrict__ views of two different buffers: the noalias scopes
+  // let hipcc's waitcnt pass see that the ds_reads need not wait for the
+  // LDS-DMA still in flight (without them it drains every DMA first).  In
+  // the steady state (DO_ISSUE) the body is one basic block and
+  // sched_group_barrier spreads the DMA issue over the first MFMAs, whose
+  // 64-cycle execution hides the address VALU.
+  auto step = [&](int kt, auto do_issue, const float* __restrict__ As, const float* __restrict__ Bs,
+                  float* __restrict__ wA, float* __restrict__ wB) {
+    constexpr bool DO_ISSUE = decltype(do_issue)::value;
+    float af[TM][HALF], bfr[TN][HALF];
+    if constexpr (DBG == 3) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int t = 0; t < HALF; ++t) af[i][t] = __builtin_amdgcn_readfirstlane(kt + t + i);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int t = 0; t < HALF; ++t) bfr[j][t] = (float)(lane + t + j);
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if constexpr (A_KC) {
+          const int row = wm0 + i * 32 + l31;
+          const int f = (row / SWZ) % QPR;
+#pragma unroll
+          for (int t = 0; t < QPR / 2; ++t) {
+            const float4 v = *reinterpret_cast<const float4*>(As + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
+            af[i][4 * t + 0] = v.x; af[i][4 * t + 1] = v.y; af[i][4 * t + 2] = v.z; af[i][4 * t + 3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < HALF; ++s) af[i][s] = As[(lh * HALF + s) * BM + wm0 + i * 32 + l31];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (B_KC) {
+          const int row = wn0 + j * 32 + l31;
+          const int f = (row / SWZ) % QPR;
+#pragma unroll
+          for (int t = 0; t < QPR / 2; ++t) {
+            const float4 v = *reinterpret_cast<const float4*>(Bs + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
+            bfr[j][4 * t + 0] = v.x; bfr[j][4 * t + 1] = v.y; bfr[j][4 * t + 2] = v.z; bfr[j][4 * t + 3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < HALF; ++s) bfr[j][s] = Bs[(lh * HALF + s) * BN + wn0 + j * 32 + l31];
+        }
+      }
+    }
+    if constexpr (DO_ISSUE && DBG != 2) issue(kt + NBUF - 1, wA, wB);
+#pragma unroll
+    for (int s = 0; s < HALF; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          if constexpr (DBG == 1) acc[i][j][s & 15] += af[i][s] * bfr[j][s];
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+    if constexpr (DO_ISSUE && UNIFORM_DMA && DBG == 0) {
+      // masks: MFMA 0x8, VALU 0x2, VMEM_READ 0x20, DS_READ 0x100
+      __builtin_amdgcn_sched_group_barrier(0x100, 64, 0);
+#pragma unroll
+      for (int d = 0; d < A_PW + B_PW; ++d) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, HALF * TM * TN, 0);
+    }
+  };
+
   if (kt0 < kt1) {
     // prologue: tiles kt0 .. kt0+NBUF-2 in flight
 #pragma unroll
@@ -420,65 +500,25 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     wait_vmcnt(per_tile * min(NBUF - 2, kt1 - kt0 - 1));
     __builtin_amdgcn_s_barrier();
     int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
+    int kt = kt0;
+    // steady state: NBUF-1 tiles in flight after this iteration's issue;
+    // tile kt+1 landed once at most (NBUF-2) tiles per wave are outstanding
+    for (; kt < kt1 - (NBUF - 1); ++kt) {
       const int nxt = cur == 0 ? NBUF - 1 : cur - 1;
-      float af[TM][HALF], bfr[TN][HALF];
-      // Reads of tile kt and the DMA of tile kt+NBUF-1 through __restrict__
-      // views of two different buffers: the noalias scopes let hipcc's
-      // waitcnt pass see that the ds_reads need not wait for the LDS-DMA
-      // still in flight (without them it drains every DMA first).
-      auto stage = [&](const float* __restrict__ As, const float* __restrict__ Bs, float* __restrict__ wA,
-                       float* __restrict__ wB) {
-        // 1) this lane's operand fragments of tile kt: LDS -> VGPRs
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          if constexpr (A_KC) {
-            const int row = wm0 + i * 32 + l31;
-            const int f = (row / SWZ) % QPR;
-#pragma unroll
-            for (int t = 0; t < QPR / 2; ++t) {
-              const float4 v = *reinterpret_cast<const float4*>(As + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
-              af[i][4 * t + 0] = v.x; af[i][4 * t + 1] = v.y; af[i][4 * t + 2] = v.z; af[i][4 * t + 3] = v.w;
-            }
-          } else {
-#pragma unroll
-            for (int s = 0; s < HALF; ++s) af[i][s] = As[(lh * HALF + s) * BM + wm0 + i * 32 + l31];
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if constexpr (B_KC) {
-            const int row = wn0 + j * 32 + l31;
-            const int f = (row / SWZ) % QPR;
-#pragma unroll
-            for (int t = 0; t < QPR / 2; ++t) {
-              const float4 v = *reinterpret_cast<const float4*>(Bs + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
-              bfr[j][4 * t + 0] = v.x; bfr[j][4 * t + 1] = v.y; bfr[j][4 * t + 2] = v.z; bfr[j][4 * t + 3] = v.w;
-            }
-          } else {
-#pragma unroll
-            for (int s = 0; s < HALF; ++s) bfr[j][s] = Bs[(lh * HALF + s) * BN + wn0 + j * 32 + l31];
-          }
-        }
-        // 2) DMA of tile kt+NBUF-1 into the buffer read in iteration kt-1
-        //    (released by the barrier that ended it)
-        if (DBG != 2 && kt + NBUF - 1 < kt1) issue(kt + NBUF - 1, wA, wB);
-      };
-      stage(smem + cur * (ASZ + BSZ), smem + cur * (ASZ + BSZ) + ASZ, smem + nxt * (ASZ + BSZ),
-            smem + nxt * (ASZ + BSZ) + ASZ);
-      // 3) MFMAs from registers while NBUF-1 tiles of DMA are in flight
-#pragma unroll
-      for (int s = 0; s < HALF; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            if constexpr (DBG == 1) acc[i][j][s & 15] += af[i][s] * bfr[j][s];
-            else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
-      // 4) tile kt+1 landed (this wave's newer DMAs may stay in flight), then
-      //    one barrier: every wave's part of tile kt+1 is in LDS and every
-      //    wave is done reading tile kt.  sched_barrier keeps hipcc from
-      //    sinking the register-only MFMAs below the wait.
+      step(kt, std::true_type{}, smem + cur * (ASZ + BSZ), smem + cur * (ASZ + BSZ) + ASZ,
+           smem + nxt * (ASZ + BSZ), smem + nxt * (ASZ + BSZ) + ASZ);
+      // sched_barrier keeps hipcc from sinking the register-only MFMAs below
+      // the wait; one barrier: every wave's part of tile kt+1 is in LDS and
+      // every wave is done reading tile kt
+      __builtin_amdgcn_sched_barrier(0);
+      wait_vmcnt(per_tile * (NBUF - 2));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      cur = cur + 1 == NBUF ? 0 : cur + 1;
+    }
+    // drain: no more DMA to issue
+    for (; kt < kt1; ++kt) {
+      step(kt, std::false_type{}, smem + cur * (ASZ + BSZ), smem + cur * (ASZ + BSZ) + ASZ, nullptr, nullptr);
       __builtin_amdgcn_sched_barrier(0);
       wait_vmcnt(per_tile * max(0, min(NBUF - 2, kt1 - kt - 2)));
       __builtin_amdgcn_s_barrier();
@@ -695,29 +735,39 @@ static size_t plan_ws(const Plan& p) {
   return p.splits > 1 ? (size_t)p.splits * (size_t)p.M * (size_t)p.N * sizeof(float) : 0;
 }
 
-template <int OP, int C>
+// Uniform-tap kernels when the reduction channel radix is a multiple of BK
+// (every layer but conv1 FWD at BK = 16; some c_out at BK = 32).
+template <int OP, int C, int DBG>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t s) {
   constexpr TileCfg t = kCfgs[C];
-  hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf>), grid, dim3(256), 0, s, a);
+  const int cred = OP == OP_FWD ? a.cp : a.cout;
+  if constexpr (OP != OP_WGRAD) {
+    if (cred % t.bk == 0) {
+      hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, DBG>), grid, dim3(256), 0, s, a);
+      return;
+    }
+  }
+  if constexpr (DBG == 0)
+    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, 0>), grid, dim3(256), 0, s, a);
 }
 
-template <int OP>
+template <int OP, int DBG = 0>
 static void launch_op(int cfg, const ConvArgs& a, dim3 grid, hipStream_t s) {
   switch (cfg) {
-    case 0: launch_cfg<OP, 0>(a, grid, s); break;
-    case 1: launch_cfg<OP, 1>(a, grid, s); break;
-    case 2: launch_cfg<OP, 2>(a, grid, s); break;
-    case 3: launch_cfg<OP, 3>(a, grid, s); break;
-    case 4: launch_cfg<OP, 4>(a, grid, s); break;
-    case 5: launch_cfg<OP, 5>(a, grid, s); break;
-    case 6: launch_cfg<OP, 6>(a, grid, s); break;
-    case 7: launch_cfg<OP, 7>(a, grid, s); break;
-    case 8: launch_cfg<OP, 8>(a, grid, s); break;
-    case 9: launch_cfg<OP, 9>(a, grid, s); break;
-    case 10: launch_cfg<OP, 10>(a, grid, s); break;
-    case 11: launch_cfg<OP, 11>(a, grid, s); break;
-    case 12: launch_cfg<OP, 12>(a, grid, s); break;
-    default: launch_cfg<OP, 13>(a, grid, s); break;
+    case 0: launch_cfg<OP, 0, DBG>(a, grid, s); break;
+    case 1: launch_cfg<OP, 1, DBG>(a, grid, s); break;
+    case 2: launch_cfg<OP, 2, DBG>(a, grid, s); break;
+    case 3: launch_cfg<OP, 3, DBG>(a, grid, s); break;
+    case 4: launch_cfg<OP, 4, DBG>(a, grid, s); break;
+    case 5: launch_cfg<OP, 5, DBG>(a, grid, s); break;
+    case 6: launch_cfg<OP, 6, DBG>(a, grid, s); break;
+    case 7: launch_cfg<OP, 7, DBG>(a, grid, s); break;
+    case 8: launch_cfg<OP, 8, DBG>(a, grid, s); break;
+    case 9: launch_cfg<OP, 9, DBG>(a, grid, s); break;
+    case 10: launch_cfg<OP, 10, DBG>(a, grid, s); break;
+    case 11: launch_cfg<OP, 11, DBG>(a, grid, s); break;
+    case 12: launch_cfg<OP, 12, DBG>(a, grid, s); break;
+    default: launch_cfg<OP, 13, DBG>(a, grid, s); break;
   }
 }
 
@@ -960,12 +1010,16 @@ JR_API int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const vo
 
 JR_API int jr_conv2d_num_configs(void) { return kNumCfgs; }
 
-// Diagnostic: time `reps` launches of one FWD GEMM of config `cfg` (0 or 3)
-// in variant dbg (0 normal, 1 no MFMA, 2 no DMA); returns ms via *ms.
+// Diagnostic: time `reps` launches of one FWD GEMM (no split-K) of tile
+// config `cfg` in variant dbg (0 normal, 1 no MFMA, 2 no DMA, 3 no LDS
+// reads); returns ms via *ms.  Results of variants 1-3 are garbage.
 JR_API int jr_conv2d_debug_time(const jr_conv_desc* d, int cfg, int dbg, const void* x, const void* w, void* y,
                                 int reps, float* ms, void* stream) {
   int rc = validate(d, OP_FWD);
   if (rc) return rc;
+  if (cfg < 0 || cfg >= kNumCfgs || dbg < 0 || dbg > 3) return fail(JR_ERR_INVALID, "debug_time: bad cfg/dbg");
+  if (dbg > 0 && chan_pad(d->c_in) % kCfgs[cfg].bk != 0)
+    return fail(JR_ERR_UNSUPPORTED, "debug_time: variants need c_in % BK == 0");
   ConvArgs a{};
   fill_common(a, d);
   a.A = (const float*)x; a.B = (const float*)w; a.C = (float*)y;
@@ -980,14 +1034,11 @@ JR_API int jr_conv2d_debug_time(const jr_conv_desc* d, int cfg, int dbg, const v
   dim3 grid(p.mt * p.nt, 1, 1);
   (void)hipEventRecord(e0, s);
   for (int r = 0; r < reps; ++r) {
-    if (cfg == 0) {
-      if (dbg == 0) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 128, 2, 16, 3, 0>), grid, dim3(256), 0, s, a);
-      if (dbg == 1) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 128, 2, 16, 3, 1>), grid, dim3(256), 0, s, a);
-      if (dbg == 2) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 128, 2, 16, 3, 2>), grid, dim3(256), 0, s, a);
-    } else {
-      if (dbg == 0) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 64, 2, 16, 4, 0>), grid, dim3(256), 0, s, a);
-      if (dbg == 1) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 64, 2, 16, 4, 1>), grid, dim3(256), 0, s, a);
-      if (dbg == 2) hipLaunchKernelGGL((k_conv<OP_FWD, 128, 64, 2, 16, 4, 2>), grid, dim3(256), 0, s, a);
+    switch (dbg) {
+      case 0: launch_op<OP_FWD, 0>(cfg, a, grid, s); break;
+      case 1: launch_op<OP_FWD, 1>(cfg, a, grid, s); break;
+      case 2: launch_op<OP_FWD, 2>(cfg, a, grid, s); break;
+      default: launch_op<OP_FWD, 3>(cfg, a, grid, s); break;
     }
   }
   (void)hipEventRecord(e1, s);
