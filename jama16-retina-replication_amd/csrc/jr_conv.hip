@@ -173,8 +173,9 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   const int kt1 = min(g.ktiles, kt0 + g.kt_per_split);
   const float* zp = g_zero_page;
   const int cred = OP == OP_FWD ? g.cp : g.cout;       // channel radix of the KC k index
-  constexpr bool ut = UT;   // wave-uniform tap: host guarantees cred % BK == 0 (not WGRAD)
-  static_assert(!(UT && OP == OP_WGRAD), "WGRAD has no uniform-tap path");
+  // FWD/DGRAD: UT = wave-uniform tap (host guarantees cred % BK == 0).
+  // WGRAD: UT = single-carry pixel counters (host guarantees wo >= BK).
+  constexpr bool ut = UT && OP != OP_WGRAD;
 
   // ---------------------------------------------------------------- A state
   const float* a_ptr[A_PW];                 // per-slot base pointer (ut paths)
@@ -291,33 +292,30 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     t_c = rc - t_r * (OP == OP_FWD ? g.kw : g.nb);
   }
 
-  const bool a_multi = A_KC ? (cred < BK) : (g.wo < BK);
+  const bool a_multi = A_KC ? (cred < BK) : (!UT && g.wo < BK);
   const bool b_multi = B_KC ? (g.cout < BK) : false;
-  auto issue = [&](int kt, float* __restrict__ As, float* __restrict__ Bs) {
-    // -------------------------------------------------------------- A
-    if constexpr (A_KC && ut) {
-      long long off;                          // wave-uniform element offset of the tap
-      int dr, dc;
-      if constexpr (OP == OP_FWD) {
-        off = (long long)(t_r * g.w + t_c) * g.xs + t_ch;
-        dr = t_r; dc = t_c;
-      } else {
-        off = -(long long)(t_r * g.wo + t_c) * g.ys + t_ch;
-        dr = -t_r; dc = -t_c;
-      }
-      const int hmax = OP == OP_FWD ? g.h : g.ho, wmax = OP == OP_FWD ? g.w : g.wo;
-#pragma unroll
-      for (int i = 0; i < A_PW; ++i) {
-        const int j = wave + 4 * i;
-        if (A_INSTR % 4 != 0 && j >= A_INSTR) continue;
+  // DMA of one operand piece (d < A_PW: A slot d, else B slot d - A_PW) of
+  // tile kt; d is a compile-time constant at every call site (unrolled), so
+  // the slot dispatch folds away.
+  auto issue_piece = [&](int kt, int d, float* __restrict__ As, float* __restrict__ Bs) {
+    if (d < A_PW) {
+      const int i = d;
+      const int j = wave + 4 * i;
+      if (A_INSTR % 4 != 0 && j >= A_INSTR) return;
+      if constexpr (A_KC && ut) {
+        long long off;                          // wave-uniform element offset of the tap
+        int dr, dc;
+        if constexpr (OP == OP_FWD) {
+          off = (long long)(t_r * g.w + t_c) * g.xs + t_ch;
+          dr = t_r; dc = t_c;
+        } else {
+          off = -(long long)(t_r * g.wo + t_c) * g.ys + t_ch;
+          dr = -t_r; dc = -t_c;
+        }
+        const int hmax = OP == OP_FWD ? g.h : g.ho, wmax = OP == OP_FWD ? g.w : g.wo;
         const bool ok = (unsigned)(a_p0[i] + dr) < (unsigned)hmax && (unsigned)(a_p1[i] + dc) < (unsigned)wmax;
         dma16(ok ? a_ptr[i] + off : zp, As + j * 256);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < A_PW; ++i) {
-        const int j = wave + 4 * i;
-        if (A_INSTR % 4 != 0 && j >= A_INSTR) continue;
+      } else {
         const float* src = zp;
         if constexpr (OP == OP_FWD) {
           const int hi = a_p0[i] + a_s0[i], wi = a_p1[i] + a_s1[i];
@@ -340,50 +338,40 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
         }
         dma16(src, As + j * 256);
       }
+      return;
     }
-    // -------------------------------------------------------------- B
+    const int i = d - A_PW;
+    const int j = wave + 4 * i;
+    if (B_INSTR % 4 != 0 && j >= B_INSTR) return;
     if constexpr (B_KC) {  // DGRAD: W[(r0+sh*a, c0+sw*bb)][ci][co]
       if constexpr (ut) {
         const long long off = (long long)((g.r0 + g.sh * t_r) * g.kw + (g.c0 + g.sw * t_c)) * g.cin * g.cout + t_ch;
-#pragma unroll
-        for (int i = 0; i < B_PW; ++i) {
-          const int j = wave + 4 * i;
-          if (B_INSTR % 4 != 0 && j >= B_INSTR) continue;
-          dma16(b_p0[i] >= 0 ? b_ptr[i] + off : zp, Bs + j * 256);
-        }
+        dma16(b_p0[i] >= 0 ? b_ptr[i] + off : zp, Bs + j * 256);
       } else {
-#pragma unroll
-        for (int i = 0; i < B_PW; ++i) {
-          const int j = wave + 4 * i;
-          if (B_INSTR % 4 != 0 && j >= B_INSTR) continue;
-          const bool ok = b_p0[i] >= 0 && b_s0[i] < g.na;
-          const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
-          const float* p = g.B + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
-          dma16(ok ? p : zp, Bs + j * 256);
-          adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
-        }
+        const bool ok = b_p0[i] >= 0 && b_s0[i] < g.na;
+        const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
+        const float* p = g.B + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
+        dma16(ok ? p : zp, Bs + j * 256);
+        adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
       }
     } else {
       const int kbase = kt * BK;                                   // wave-uniform
       const long long off = (long long)(kbase - kt0 * BK) * (OP == OP_FWD ? g.N : g.ys);
-#pragma unroll
-      for (int i = 0; i < B_PW; ++i) {
-        const int j = wave + 4 * i;
-        if (B_INSTR % 4 != 0 && j >= B_INSTR) continue;
-        const int k = b_s0[i] + (kbase - kt0 * BK);
-        bool ok = b_p0[i] >= 0 && k < g.K;
-        const float* p = b_ptr[i] + off;
-        if constexpr (OP == OP_FWD) {
-          if (!ut && g.cp != g.cin) {  // virtual channel padding (c_in % 4 != 0): uniform branch
-            const int rc = k / g.cp, ci = k - rc * g.cp;
-            ok = ok && ci < g.cin;
-            p = g.B + ((rc * g.cin + ci) * g.N + b_p0[i]);
-          }
+      const int k = b_s0[i] + (kbase - kt0 * BK);
+      bool ok = b_p0[i] >= 0 && k < g.K;
+      const float* p = b_ptr[i] + off;
+      if constexpr (OP == OP_FWD) {
+        if (!ut && g.cp != g.cin) {  // virtual channel padding (c_in % 4 != 0): uniform branch
+          const int rc = k / g.cp, ci = k - rc * g.cp;
+          ok = ok && ci < g.cin;
+          p = g.B + ((rc * g.cin + ci) * g.N + b_p0[i]);
         }
-        dma16(ok ? p : zp, Bs + j * 256);
       }
+      dma16(ok ? p : zp, Bs + j * 256);
     }
-    // advance the wave-uniform tap by BK
+  };
+  // advance the wave-uniform tap by BK after a tile's pieces are issued
+  auto advance = [&]() {
     if constexpr (ut) {   // branch-free (s_cselect) so the K loop stays one basic block
       t_ch += BK;
       const bool w1 = t_ch == cred;
@@ -393,6 +381,12 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       t_c = w2 ? 0 : t_c;
       t_r += w2 ? 1 : 0;
     }
+  };
+  constexpr int NPIECE = A_PW + B_PW;
+  auto issue = [&](int kt, float* __restrict__ As, float* __restrict__ Bs) {
+#pragma unroll
+    for (int d = 0; d < NPIECE; ++d) issue_piece(kt, d, As, Bs);
+    advance();
   };
 
   f32x16 acc[TM][TN];
@@ -404,27 +398,20 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int l31 = lane & 31, lh = lane >> 5;
-  // DMA wave-instructions this wave issues per K-tile (wave-uniform; a
-  // compile-time constant when every wave issues the same number)
-  constexpr bool UNIFORM_DMA = (A_INSTR % 4 == 0) && (B_INSTR % 4 == 0);
-  int per_tile = A_INSTR / 4 + B_INSTR / 4;
-  if constexpr (!UNIFORM_DMA) {
-    per_tile = 0;
-#pragma unroll
-    for (int i = 0; i < A_PW; ++i) per_tile += (wave + 4 * i < A_INSTR);
-#pragma unroll
-    for (int i = 0; i < B_PW; ++i) per_tile += (wave + 4 * i < B_INSTR);
-  }
+  // DMA wave-instructions per K-tile used for the counted waits: the
+  // minimum over the block's waves, a compile-time constant.  A wave that
+  // issues one more piece per tile (A_INSTR or B_INSTR not a multiple of 4)
+  // then waits for one piece of a newer tile too — safe, and it keeps the
+  // K loop free of per-wave branches.
+  constexpr int per_tile = A_INSTR / 4 + B_INSTR / 4;
 
-  // One K-tile: fragments of tile kt (LDS -> VGPRs), DMA of tile
-  // kt+NBUF-1 into the buffer read in iteration kt-1 (released by the
-  // barrier that ended it), MFMAs from registers.  The reads and the DMA go
-  // through __restrict__ views of two different buffers: the noalias scopes
-  // let hipcc's waitcnt pass see that the ds_reads need not wait for the
-  // LDS-DMA still in flight (without them it drains every DMA first).  In
-  // the steady state (DO_ISSUE) the body is one basic block and
-  // sched_group_barrier spreads the DMA issue over the first MFMAs, whose
-  // 64-cycle execution hides the address VALU.
+  // One K-tile: fragments of tile kt (LDS -> VGPRs), then MFMAs from
+  // registers with the DMA of tile kt+NBUF-1 (into the buffer read in
+  // iteration kt-1, released by the barrier that ended it) issued piece by
+  // piece between the k-steps.  The reads and the DMA go through
+  // __restrict__ views of two different buffers: the noalias scopes let
+  // hipcc's waitcnt pass see that the ds_reads need not wait for the LDS-DMA
+  // still in flight (without them it drains every DMA first).
   auto step = [&](int kt, auto do_issue, const float* __restrict__ As, const float* __restrict__ Bs,
                   float* __restrict__ wA, float* __restrict__ wB) {
     constexpr bool DO_ISSUE = decltype(do_issue)::value;
@@ -470,25 +457,24 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
         }
       }
     }
-    if constexpr (DO_ISSUE && DBG != 2) issue(kt + NBUF - 1, wA, wB);
+    // MFMAs of k-step s, then DMA piece s of tile kt+NBUF-1: program order
+    // places each piece's address VALU and issue under an MFMA group in
+    // flight (the LDS-DMA intrinsic is a scheduling boundary for hipcc).
 #pragma unroll
-    for (int s = 0; s < HALF; ++s)
+    for (int s = 0; s < HALF; ++s) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           if constexpr (DBG == 1) acc[i][j][s & 15] += af[i][s] * bfr[j][s];
           else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
-    if constexpr (DO_ISSUE && UNIFORM_DMA && DBG == 0) {
-      // masks: MFMA 0x8, VALU 0x2, VMEM_READ 0x20, DS_READ 0x100
-      __builtin_amdgcn_sched_group_barrier(0x100, 64, 0);
+      if constexpr (DO_ISSUE && DBG != 2)
+        if (s < NPIECE) issue_piece(kt + NBUF - 1, s, wA, wB);
+    }
+    if constexpr (DO_ISSUE && DBG != 2) {
 #pragma unroll
-      for (int d = 0; d < A_PW + B_PW; ++d) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, HALF * TM * TN, 0);
+      for (int d = HALF; d < NPIECE; ++d) issue_piece(kt + NBUF - 1, d, wA, wB);
+      advance();
     }
   };
 
@@ -735,17 +721,15 @@ static size_t plan_ws(const Plan& p) {
   return p.splits > 1 ? (size_t)p.splits * (size_t)p.M * (size_t)p.N * sizeof(float) : 0;
 }
 
-// Uniform-tap kernels when the reduction channel radix is a multiple of BK
-// (every layer but conv1 FWD at BK = 16; some c_out at BK = 32).
+// Fast-path kernels (UT): FWD/DGRAD when the reduction channel radix is a
+// multiple of BK (every layer but conv1 FWD at BK = 16); WGRAD when wo >= BK.
 template <int OP, int C, int DBG>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t s) {
   constexpr TileCfg t = kCfgs[C];
-  const int cred = OP == OP_FWD ? a.cp : a.cout;
-  if constexpr (OP != OP_WGRAD) {
-    if (cred % t.bk == 0) {
-      hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, DBG>), grid, dim3(256), 0, s, a);
-      return;
-    }
+  const bool fast = OP == OP_WGRAD ? a.wo >= t.bk : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
+  if (fast) {
+    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, DBG>), grid, dim3(256), 0, s, a);
+    return;
   }
   if constexpr (DBG == 0)
     hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, 0>), grid, dim3(256), 0, s, a);
