@@ -79,11 +79,17 @@ const char* jr_version(void);
 /* ---- convolution (train.py:129-130 -> Keras Conv2D -> TF Conv2D,
  *      Conv2DBackpropInput, Conv2DBackpropFilter created by .minimize at
  *      train.py:150-153) ----------------------------------------------- */
-/* c_out must be a multiple of 16.  c_in % 4 != 0 (the 3-channel image of
- * conv1) is supported for fwd / bwd_filter by virtual padding to
- * c4 = round_up(c_in, 4): the input buffer must hold c4 channels per pixel
- * (x_c_off + c4 <= x_c_stride) and channels [c_in, c4) must be finite
- * (zero); the kernel tensor stays [kh][kw][c_in][c_out]. */
+/* c_out must be a multiple of 16.  Channel offsets/strides are multiples
+ * of q = 4 (JR_F32) or 8 (JR_BF16) elements (one 16 B DMA piece).  c_in % q
+ * != 0 (the 3-channel image of conv1) is supported for fwd / bwd_filter by
+ * virtual padding to cq = round_up(c_in, q): the input buffer must hold cq
+ * channels per pixel (x_c_off + cq <= x_c_stride) and channels [c_in, cq)
+ * must be finite (zero).
+ * Filter layouts: JR_F32 fwd / bwd_data and JR_BF16 bwd_data take the HWIO
+ * kernel [kh][kw][c_in][c_out]; JR_BF16 fwd takes it transposed and padded,
+ * [c_out][kh][kw][cq] (jr_conv_weights_bf16 produces both bf16 layouts);
+ * bwd_filter writes fp32 HWIO for both dtypes.  JR_BF16 activations,
+ * outputs and dx are bf16 (accumulation in fp32 MFMA, rounded once). */
 size_t jr_conv2d_workspace_size(const jr_conv_desc* d, int op, int dtype);
 /* y[.., y_c_off + co] = sum x * w   (raw conv output, no bias) */
 int jr_conv2d_fwd(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y,
@@ -102,10 +108,11 @@ int jr_conv2d_bwd_filter(const jr_conv_desc* d, int dtype, const void* x, const 
 int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const void* a, const void* b, void* c,
                        void* ws, size_t ws_bytes, void* stream);
 /* Tile configuration the next call would use (DGRAD: per stride phase),
- * and an explicit override (reproducibility, tests). */
-int jr_conv2d_get_config(const jr_conv_desc* d, int op, int phase);
-int jr_conv2d_set_config(const jr_conv_desc* d, int op, int phase, int cfg);
-int jr_conv2d_num_configs(void);
+ * and an explicit override (reproducibility, tests).  A config id is
+ * tile | (splits << 8), splits = 0: planner's split-K factor. */
+int jr_conv2d_get_config(const jr_conv_desc* d, int op, int dtype, int phase);
+int jr_conv2d_set_config(const jr_conv_desc* d, int op, int dtype, int phase, int cfg);
+int jr_conv2d_num_configs(int dtype);   /* tiles of that dtype's table */
 
 /* ---- BatchNormalization(scale=False, eps) + ReLU, training-mode batch
  *      statistics (Keras conv2d_bn; App. C Q1: always batch stats) ----- */
@@ -163,6 +170,26 @@ int jr_sgd_update(float* w, const float* grad, int64_t n, float lr, float grad_s
 /* Adam (north-star extra, not in the reference): TF AdamOptimizer form */
 int jr_adam_update(float* w, const float* grad, float* m, float* v, int64_t n, float lr_t,
                    float beta1, float beta2, float eps, float grad_scale, void* stream);
+
+/* ---- bf16 filter copies (the bf16 conv path's weight operands) -------
+ * From the fp32 master kernel [kh][kw][c_in][c_out] write
+ *   w_hwio: bf16 [kh][kw][c_in][c_out]        (jr_conv2d_bwd_data, JR_BF16)
+ *   w_t:    bf16 [c_out][kh][kw][c8], c8 = round_up(c_in, 8), zero padded
+ *           (jr_conv2d_fwd, JR_BF16)
+ * Either output may be NULL.  The _multi form does every layer of a model
+ * in one launch from a DEVICE array of jr_wprep (offsets in elements from
+ * the three bases; tile_start = exclusive prefix sum of
+ * jr_conv_weights_bf16_tiles over the layers). */
+typedef struct jr_wprep {
+  int64_t src_off, hwio_off, wt_off;
+  int32_t kh, kw, c_in, c_out;
+  int32_t tile_start, reserved;
+} jr_wprep;
+int32_t jr_conv_weights_bf16_tiles(int32_t kh, int32_t kw, int32_t c_in, int32_t c_out);
+int jr_conv_weights_bf16(const float* w, int32_t kh, int32_t kw, int32_t c_in, int32_t c_out, void* w_hwio,
+                         void* w_t, void* stream);
+int jr_conv_weights_bf16_multi(const jr_wprep* layers, int32_t n_layers, int32_t total_tiles, const float* src,
+                               void* hwio, void* wt, void* stream);
 
 /* ---- dtype helpers --------------------------------------------------- */
 int jr_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream);

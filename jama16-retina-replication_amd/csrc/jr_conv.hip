@@ -33,7 +33,7 @@
 // k runs over (r, c, ci4 < 4); the input buffer must hold 4 readable
 // (finite; the engine keeps them zero) channels per pixel and the weight
 // rows ci4 >= c_in read as zeros.
-#include "jr_common.h"
+#include "jr_conv_impl.h"
 
 #include <array>
 #include <type_traits>
@@ -41,95 +41,6 @@
 #include <mutex>
 
 namespace jr {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-enum { OP_FWD = 0, OP_DGRAD = 1, OP_WGRAD = 2 };
-
-// 64 B of zeros in global memory: the DMA source of out-of-bounds taps.
-__device__ __attribute__((aligned(64))) float g_zero_page[16];
-
-struct ConvArgs {
-  const float* A;
-  const float* B;
-  float* C;
-  int M, N, K;                // GEMM dims (DGRAD: of this phase)
-  int n, h, w, cin, cp, cout, kh, kw, sh, sw, ph, pw, ho, wo;
-  int xo, xs, yo, ys;         // channel slices of x and of dy
-  int c_off, c_stride;        // output addressing
-  int accumulate;
-  int ktiles, kt_per_split, ntn;
-  long long slab_elems;       // M*N (split-K slabs)
-  // DGRAD phase (py,px): taps r = r0 + sh*a (a < na), c = c0 + sw*b (b < nb);
-  // m = (b, u, v) over hc x wc; ih = sh*u + py; oh = u + ey - a.
-  int py, px, r0, c0, na, nb, ey, ex, hc, wc;
-};
-
-// Output element offset of GEMM row m (column 0), or -1 to drop the row.
-template <int OP>
-__device__ __forceinline__ long long out_row(const ConvArgs& g, int m) {
-  if constexpr (OP == OP_FWD) {
-    return (long long)m * g.c_stride + g.c_off;
-  } else if constexpr (OP == OP_DGRAD) {
-    const int hw = g.hc * g.wc;
-    const int b = m / hw, rem = m - b * hw;
-    const int u = rem / g.wc, v = rem - u * g.wc;
-    const long long pix = ((long long)b * g.h + g.sh * u + g.py) * g.w + g.sw * v + g.px;
-    return pix * g.c_stride + g.c_off;
-  } else {
-    if (g.cp == g.cin) return (long long)m * g.N;
-    const int rc = m / g.cp, ci = m - rc * g.cp;
-    if (ci >= g.cin) return -1;
-    return ((long long)rc * g.cin + ci) * g.N;
-  }
-}
-
-// s_waitcnt vmcnt(n) + lgkmcnt(0) for a wave-uniform runtime n (immediate
-// operand: switch over the values a K-tile pipeline can need).
-__device__ __forceinline__ void wait_vmcnt(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
-  }
-}
-
-// Advance the mixed-radix counter (z, y, x) (radices ly, lx) by BK along x.
-// multi (wave-uniform) = lx < BK: more than one carry is possible.
-template <int BK>
-__device__ __forceinline__ void adv_mixed_t(int& x, int& y, int& z, int lx, int ly, bool multi) {
-  x += BK;
-  if (!multi) {
-    const bool c1 = x >= lx;
-    x = c1 ? x - lx : x;
-    y += c1 ? 1 : 0;
-    const bool c2 = y == ly;
-    y = c2 ? 0 : y;
-    z += c2 ? 1 : 0;
-  } else {
-    while (x >= lx) {
-      x -= lx;
-      if (++y == ly) { y = 0; ++z; }
-    }
-  }
-}
-#define adv_mixed(x, y, z, lx, ly, multi) adv_mixed_t<BK>(x, y, z, lx, ly, multi)
-
-__device__ __forceinline__ void dma16(const float* src, float* lds_chunk) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_chunk, 16, 0, 0);
-}
 
 // DBG (diagnostic builds only, jr_conv2d_debug_time): 1 = no MFMA,
 // 2 = no DMA after the first tile (results are wrong in both).
@@ -537,91 +448,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   }
 }
 
-// out[out_row(m) + n] (+)= sum_z slab[z][m][n], float4 along n (N % 16 == 0
-// and channel offsets/strides % 4 == 0 keep every access 16-byte aligned).
-// Block = G z-lanes x (256 / G) float4 columns: z-lane zg sums slabs zg,
-// zg + G, ... and the G lane sums are added in zg order through LDS, so the
-// result depends only on (M, N, splits), never on timing.  G grows when
-// M*N is small and splits large (the wgrad case: a few thousand outputs, up
-// to 256 slabs) so the reduce still spreads over the whole chip.
-template <int OP>
-__global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ slab, int splits, int G,
-                                                       ConvArgs g, float* out) {
-  __shared__ float4 part[256];
-  const int cols = 256 / G;
-  const int t = threadIdx.x;
-  const int zg = t / cols, cl = t - zg * cols;
-  const int n4 = g.N >> 2;
-  const long long total = (long long)g.M * n4;
-  const long long zs = g.slab_elems >> 2;
-  for (long long e0 = (long long)blockIdx.x * cols; e0 < total; e0 += (long long)gridDim.x * cols) {
-    const long long e = e0 + cl;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e < total) {
-      const float4* src = reinterpret_cast<const float4*>(slab) + e;
-      int z = zg;
-      for (; z + 3 * G < splits; z += 4 * G) {
-        const float4 a = src[z * zs], b = src[(z + G) * zs], c = src[(z + 2 * G) * zs], d = src[(z + 3 * G) * zs];
-        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
-        s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
-        s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
-        s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
-      }
-      for (; z < splits; z += G) {
-        const float4 a = src[z * zs];
-        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
-      }
-    }
-    if (G > 1) {
-      part[t] = s;
-      __syncthreads();
-      if (zg == 0) {
-        for (int k = 1; k < G; ++k) {
-          const float4 a = part[k * cols + cl];
-          s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
-        }
-      }
-      __syncthreads();
-    }
-    if (zg != 0 || e >= total) continue;
-    const int m = (int)(e / n4), q = (int)(e - (long long)m * n4);
-    const long long base = out_row<OP>(g, m);
-    if (base < 0) continue;
-    float4* p = reinterpret_cast<float4*>(out + base + q * 4);
-    if (g.accumulate) {
-      const float4 o = *p;
-      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
-    }
-    *p = s;
-  }
-}
-
 // ---------------------------------------------------------------- host side
-struct TileCfg {
-  int bm, bn, wgm, bk, nbuf;
-  double eff;  // relative MFMA efficiency guess used to rank padded work
-};
-
-// Candidate tiles (block BMxBN, WGM waves along M, K-tile BK).  The planner
-// ranks them by padded work / eff; jr_conv2d_autotune times them instead.
-// Keep in sync with launch_op's switch.
-static constexpr TileCfg kCfgs[] = {
-    {128, 128, 2, 16, 3, 1.00},  // 0: wave 64x64, 48 KiB LDS
-    {128, 128, 2, 32, 2, 1.00},  // 1: 64 KiB
-    {256, 64, 4, 16, 3, 1.00},   // 2: wave 64x64, 60 KiB
-    {128, 64, 2, 16, 4, 0.92},   // 3: wave 64x32, 48 KiB
-    {128, 64, 2, 32, 2, 0.92},   // 4: 48 KiB
-    {128, 96, 4, 16, 3, 0.90},   // 5: wave 32x96, 42 KiB
-    {256, 32, 4, 16, 4, 0.85},   // 6: wave 64x32, 72 KiB
-    {64, 64, 2, 32, 3, 0.75},    // 7: wave 32x32, 48 KiB
-    {128, 32, 4, 32, 3, 0.75},   // 8: wave 32x32, 60 KiB
-    {64, 128, 2, 32, 2, 0.80},   // 9: wave 32x64, 48 KiB
-    {128, 64, 2, 16, 2, 0.90},   // 10: wave 64x32, 24 KiB
-    {128, 192, 2, 16, 3, 1.02},  // 11: wave 64x96, 60 KiB (N = 192 layers)
-    {256, 96, 4, 16, 3, 1.02},   // 12: wave 64x96, 66 KiB (N = 96 layers)
-    {256, 128, 2, 16, 3, 1.04},  // 13: wave 128x64, 72 KiB
-};
-constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
 struct Phase {
   int py, px, r0, c0, na, nb, ey, ex, hc, wc;
@@ -640,7 +467,14 @@ struct Plan {
   int mt, nt, ktiles, splits, kt_per_split;
 };
 
-static int chan_pad(int c) { return (c + 3) / 4 * 4; }
+// Channel padding of the reduction operand: 16 B DMA pieces hold 4 fp32 or
+// 8 bf16 channels.
+static int chan_pad(int c, int dtype) {
+  const int q = dtype == JR_BF16 ? 8 : 4;
+  return (c + q - 1) / q * q;
+}
+static const TileCfg* cfg_table(int dtype) { return dtype == JR_BF16 ? kCfgsBf16 : kCfgs; }
+static int cfg_count(int dtype) { return dtype == JR_BF16 ? kNumCfgsBf16 : kNumCfgs; }
 
 static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
   int k = 0;
@@ -662,10 +496,10 @@ static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
   *nph = k;
 }
 
-static Plan plan_with(int cfg, int M, int N, int K) {
+static Plan plan_with(int dtype, int cfg, int M, int N, int K) {
   Plan p{};
   p.M = M; p.N = N; p.K = K; p.cfg = cfg; p.tile = cfg_tile(cfg);
-  const TileCfg& t = kCfgs[p.tile];
+  const TileCfg& t = cfg_table(dtype)[p.tile];
   p.mt = (int)ceil_div(M, t.bm);
   p.nt = (int)ceil_div(N, t.bn);
   p.ktiles = (int)ceil_div(K, t.bk);
@@ -683,11 +517,11 @@ static Plan plan_with(int cfg, int M, int N, int K) {
   return p;
 }
 
-static int heuristic_cfg(int M, int N, int K) {
+static int heuristic_cfg(int dtype, int M, int N, int K) {
   double best = 1e300;
   int bc = 0;
-  for (int c = 0; c < kNumCfgs; ++c) {
-    const TileCfg& t = kCfgs[c];
+  for (int c = 0; c < cfg_count(dtype); ++c) {
+    const TileCfg& t = cfg_table(dtype)[c];
     const double tiles = (double)ceil_div(M, t.bm) * ceil_div(N, t.bn);
     double work = tiles * t.bm * t.bn / t.eff;
     // grids that cannot fill the 256 CUs and cannot be split along K lose
@@ -698,23 +532,23 @@ static int heuristic_cfg(int M, int N, int K) {
 }
 
 // Autotune cache: (op, GEMM dims, conv geometry) -> best config.
-typedef std::array<int, 12> TuneKey;
+typedef std::array<int, 13> TuneKey;
 static std::mutex g_tune_mu;
 static std::map<TuneKey, int> g_tuned;
 
-static TuneKey tune_key(int op, int M, int N, int K, const jr_conv_desc* d) {
-  return TuneKey{op, M, N, K, d->h, d->w, d->kh, d->kw, d->stride_h, d->c_in, d->c_out, d->n};
+static TuneKey tune_key(int dtype, int op, int M, int N, int K, const jr_conv_desc* d) {
+  return TuneKey{dtype, op, M, N, K, d->h, d->w, d->kh, d->kw, d->stride_h, d->c_in, d->c_out, d->n};
 }
 
-static Plan make_plan(int op, int M, int N, int K, const jr_conv_desc* d, int force_cfg = -1) {
+static Plan make_plan(int dtype, int op, int M, int N, int K, const jr_conv_desc* d, int force_cfg = -1) {
   int cfg = force_cfg;
   if (cfg < 0) {
     std::lock_guard<std::mutex> lk(g_tune_mu);
-    auto it = g_tuned.find(tune_key(op, M, N, K, d));
+    auto it = g_tuned.find(tune_key(dtype, op, M, N, K, d));
     if (it != g_tuned.end()) cfg = it->second;
   }
-  if (cfg < 0) cfg = heuristic_cfg(M, N, K);
-  return plan_with(cfg, M, N, K);
+  if (cfg < 0) cfg = heuristic_cfg(dtype, M, N, K);
+  return plan_with(dtype, cfg, M, N, K);
 }
 
 static size_t plan_ws(const Plan& p) {
@@ -755,7 +589,9 @@ static void launch_op(int cfg, const ConvArgs& a, dim3 grid, hipStream_t s) {
   }
 }
 
-static int validate(const jr_conv_desc* d, int op) {
+static int validate(const jr_conv_desc* d, int op, int dtype) {
+  if (dtype != JR_F32 && dtype != JR_BF16) return fail(JR_ERR_INVALID, "conv: bad dtype");
+  const int q = dtype == JR_BF16 ? 8 : 4;   // channels per 16 B piece
   if (!d) return fail(JR_ERR_INVALID, "conv: null descriptor");
   if (op < OP_FWD || op > OP_WGRAD) return fail(JR_ERR_INVALID, "conv: bad op");
   if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c_in <= 0 || d->c_out <= 0 || d->kh <= 0 ||
@@ -767,17 +603,17 @@ static int validate(const jr_conv_desc* d, int op) {
     return fail(JR_ERR_INVALID, "conv: ho/wo inconsistent with h,w,k,stride,pad");
   if (d->pad_h >= d->kh || d->pad_w >= d->kw)
     return fail(JR_ERR_INVALID, "conv: padding must be smaller than the kernel");
-  const int cp = chan_pad(d->c_in);
+  const int cp = chan_pad(d->c_in, dtype);
   if (d->x_c_off < 0 || d->x_c_off + cp > d->x_c_stride)
-    return fail(JR_ERR_INVALID, "conv: input channel slice (padded to a multiple of 4) out of range");
+    return fail(JR_ERR_INVALID, "conv: input channel slice (padded to 4 fp32 / 8 bf16 channels) out of range");
   if (d->y_c_off < 0 || d->y_c_off + d->c_out > d->y_c_stride)
     return fail(JR_ERR_INVALID, "conv: output channel slice out of range");
   if (d->c_out % 16 != 0)
     return fail(JR_ERR_UNSUPPORTED, "conv: c_out must be a multiple of 16");
-  if (d->x_c_off % 4 || d->x_c_stride % 4 || d->y_c_off % 4 || d->y_c_stride % 4)
-    return fail(JR_ERR_INVALID, "conv: channel offsets and strides must be multiples of 4");
-  if (op == OP_DGRAD && d->c_in % 4 != 0)
-    return fail(JR_ERR_UNSUPPORTED, "conv bwd_data: c_in must be a multiple of 4");
+  if (d->x_c_off % q || d->x_c_stride % q || d->y_c_off % q || d->y_c_stride % q)
+    return fail(JR_ERR_INVALID, "conv: channel offsets and strides must be multiples of 4 (fp32) / 8 (bf16)");
+  if (op == OP_DGRAD && d->c_in % q != 0)
+    return fail(JR_ERR_UNSUPPORTED, "conv bwd_data: c_in must be a multiple of 4 (fp32) / 8 (bf16)");
   if (d->stride_h * d->stride_w > 64) return fail(JR_ERR_UNSUPPORTED, "conv: stride too large");
   const long long xin = (long long)d->n * d->h * d->w * d->x_c_stride;
   const long long yout = (long long)d->n * d->ho * d->wo * d->y_c_stride;
@@ -787,8 +623,8 @@ static int validate(const jr_conv_desc* d, int op) {
   return JR_OK;
 }
 
-static void fill_common(ConvArgs& a, const jr_conv_desc* d) {
-  a.n = d->n; a.h = d->h; a.w = d->w; a.cin = d->c_in; a.cp = chan_pad(d->c_in); a.cout = d->c_out;
+static void fill_common(ConvArgs& a, const jr_conv_desc* d, int dtype) {
+  a.n = d->n; a.h = d->h; a.w = d->w; a.cin = d->c_in; a.cp = chan_pad(d->c_in, dtype); a.cout = d->c_out;
   a.kh = d->kh; a.kw = d->kw; a.sh = d->stride_h; a.sw = d->stride_w;
   a.ph = d->pad_h; a.pw = d->pad_w; a.ho = d->ho; a.wo = d->wo;
   a.xo = d->x_c_off; a.xs = d->x_c_stride; a.yo = d->y_c_off; a.ys = d->y_c_stride;
@@ -796,7 +632,7 @@ static void fill_common(ConvArgs& a, const jr_conv_desc* d) {
 
 // One GEMM (plus its split-K reduce) on the stream.
 template <int OP>
-static int run_gemm(ConvArgs a, const Plan& p, float* out, void* ws, size_t ws_bytes, hipStream_t s) {
+static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, size_t ws_bytes, hipStream_t s) {
   if (p.M <= 0 || p.N <= 0) return JR_OK;
   a.M = p.M; a.N = p.N; a.K = p.K;
   a.ktiles = p.ktiles;
@@ -807,10 +643,16 @@ static int run_gemm(ConvArgs a, const Plan& p, float* out, void* ws, size_t ws_b
     if (!ws || ws_bytes < plan_ws(p)) return fail(JR_ERR_WORKSPACE, "conv: workspace too small for split-K");
     a.C = static_cast<float*>(ws);
   } else {
-    a.C = out;
+    a.C = static_cast<float*>(out);
   }
   dim3 grid(p.mt * p.nt, 1, p.splits);
-  launch_op<OP>(p.tile, a, grid, s);
+  if (dtype == JR_BF16) {
+    const TileCfg& t = kCfgsBf16[p.tile];
+    const bool fast = OP == OP_WGRAD ? a.wo >= t.bk : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
+    launch_conv_bf16(OP, p.tile, fast, a, grid, s);
+  } else {
+    launch_op<OP>(p.tile, a, grid, s);
+  }
   int rc = check_launch("conv gemm");
   if (rc || p.splits <= 1) return rc;
   const long long total = (long long)p.M * p.N / 4;   // float4 columns
@@ -818,34 +660,39 @@ static int run_gemm(ConvArgs a, const Plan& p, float* out, void* ws, size_t ws_b
   while (G < 64 && G * 4 <= p.splits && total * G < 128 * 1024) G *= 2;
   const long long cols = 256 / G;
   const int blocks = (int)std::min<long long>(ceil_div(total, cols), 8192);
-  hipLaunchKernelGGL((k_splitk_reduce<OP>), dim3(blocks), dim3(256), 0, s, (const float*)ws, p.splits, G, a, out);
+  if (dtype == JR_BF16 && OP != OP_WGRAD)   // bf16 activations / activation grads; dW stays fp32
+    hipLaunchKernelGGL((k_splitk_reduce<OP, uint16_t>), dim3(blocks), dim3(256), 0, s, (const float*)ws, p.splits,
+                       G, a, static_cast<uint16_t*>(out));
+  else
+    hipLaunchKernelGGL((k_splitk_reduce<OP, float>), dim3(blocks), dim3(256), 0, s, (const float*)ws, p.splits, G,
+                       a, static_cast<float*>(out));
   return check_launch("conv split-k reduce");
 }
 
-static void gemm_dims(const jr_conv_desc* d, int op, const Phase* ph, int* M, int* N, int* K) {
-  const int cp = chan_pad(d->c_in);
+static void gemm_dims(const jr_conv_desc* d, int op, int dtype, const Phase* ph, int* M, int* N, int* K) {
+  const int cp = chan_pad(d->c_in, dtype);
   if (op == OP_FWD) { *M = d->n * d->ho * d->wo; *N = d->c_out; *K = d->kh * d->kw * cp; }
   else if (op == OP_WGRAD) { *M = d->kh * d->kw * cp; *N = d->c_out; *K = d->n * d->ho * d->wo; }
   else { *M = d->n * ph->hc * ph->wc; *N = d->c_in; *K = ph->na * ph->nb * d->c_out; }
 }
 
-static Plan plan_for(const jr_conv_desc* d, int op, const Phase* ph, int force_cfg = -1) {
+static Plan plan_for(const jr_conv_desc* d, int op, int dtype, const Phase* ph, int force_cfg = -1) {
   int M, N, K;
-  gemm_dims(d, op, ph, &M, &N, &K);
-  return make_plan(op, M, N, K, d, force_cfg);
+  gemm_dims(d, op, dtype, ph, &M, &N, &K);
+  return make_plan(dtype, op, M, N, K, d, force_cfg);
 }
 
 // Workspace: twice the max over every candidate tile's planned split-K, so
 // any tuned choice fits.
-static size_t ws_bytes_for(const jr_conv_desc* d, int op) {
+static size_t ws_bytes_for(const jr_conv_desc* d, int op, int dtype) {
   Phase ph[64];
   int nph = 1;
   if (op == OP_DGRAD) dgrad_phases(d, ph, &nph);
   size_t w = 0;
   for (int i = 0; i < nph; ++i) {
     if (op == OP_DGRAD && (ph[i].na == 0 || ph[i].nb == 0 || ph[i].hc == 0 || ph[i].wc == 0)) continue;
-    for (int c = 0; c < kNumCfgs; ++c)
-      w = std::max(w, plan_ws(plan_for(d, op, op == OP_DGRAD ? &ph[i] : nullptr, c)));
+    for (int c = 0; c < cfg_count(dtype); ++c)
+      w = std::max(w, plan_ws(plan_for(d, op, dtype, op == OP_DGRAD ? &ph[i] : nullptr, c)));
   }
   return 2 * w;   // room for the autotuner's doubled split-K factors
 }
@@ -854,26 +701,25 @@ static size_t ws_bytes_for(const jr_conv_desc* d, int op) {
 static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, const void* B, void* C,
                     int accumulate, void* ws, size_t ws_bytes, void* stream, int force_cfg = -1,
                     int only_phase = -1) {
-  int rc = validate(d, op);
+  int rc = validate(d, op, dtype);
   if (rc) return rc;
-  if (dtype != JR_F32) return fail(JR_ERR_UNSUPPORTED, "conv: bf16 path not built in this round");
   if (!A || !B || !C) return fail(JR_ERR_INVALID, "conv: null tensor pointer");
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15)
     return fail(JR_ERR_INVALID, "conv: tensors must be 16-byte aligned");
   ConvArgs a{};
-  fill_common(a, d);
-  a.A = static_cast<const float*>(A);
+  fill_common(a, d, dtype);
+  a.A = static_cast<const float*>(A);   // bf16 kernels reinterpret
   a.B = static_cast<const float*>(B);
   a.accumulate = accumulate;
   hipStream_t s = as_stream(stream);
-  float* out = static_cast<float*>(C);
+  void* out = C;
   if (op == OP_FWD) {
     a.c_off = d->y_c_off; a.c_stride = d->y_c_stride;
-    return run_gemm<OP_FWD>(a, plan_for(d, op, nullptr, force_cfg), out, ws, ws_bytes, s);
+    return run_gemm<OP_FWD>(dtype, a, plan_for(d, op, dtype, nullptr, force_cfg), out, ws, ws_bytes, s);
   }
   if (op == OP_WGRAD) {
     a.c_off = 0; a.c_stride = d->c_out;
-    return run_gemm<OP_WGRAD>(a, plan_for(d, op, nullptr, force_cfg), out, ws, ws_bytes, s);
+    return run_gemm<OP_WGRAD>(dtype, a, plan_for(d, op, dtype, nullptr, force_cfg), out, ws, ws_bytes, s);
   }
   Phase ph[64];
   int nph = 0;
@@ -889,12 +735,12 @@ static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, con
     if (p.na == 0 || p.nb == 0) {
       // no tap reaches this phase: a K = 0 GEMM stores zeros (or leaves dx)
       if (accumulate) continue;
-      pl = plan_with(heuristic_cfg(d->n * p.hc * p.wc, d->c_in, 16), d->n * p.hc * p.wc, d->c_in, 16);
+      pl = plan_with(dtype, heuristic_cfg(dtype, d->n * p.hc * p.wc, d->c_in, 16), d->n * p.hc * p.wc, d->c_in, 16);
       pl.K = 0; pl.ktiles = 0; pl.splits = 1; pl.kt_per_split = 1;
     } else {
-      pl = plan_for(d, op, &p, force_cfg);
+      pl = plan_for(d, op, dtype, &p, force_cfg);
     }
-    rc = run_gemm<OP_DGRAD>(a, pl, out, ws, ws_bytes, s);
+    rc = run_gemm<OP_DGRAD>(dtype, a, pl, out, ws, ws_bytes, s);
     if (rc) return rc;
   }
   return JR_OK;
@@ -904,7 +750,7 @@ static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, con
 // the caller's buffers (outputs are overwritten) and remember the fastest.
 static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, const void* B, void* C, void* ws,
                     size_t ws_bytes, void* stream, int reps) {
-  int rc = validate(d, op);
+  int rc = validate(d, op, dtype);
   if (rc) return rc;
   Phase ph[64];
   int nph = 1;
@@ -916,11 +762,12 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
   for (int i = 0; i < nph; ++i) {
     if (op == OP_DGRAD && (ph[i].na == 0 || ph[i].nb == 0 || ph[i].hc == 0 || ph[i].wc == 0)) continue;
     int M, N, K;
-    gemm_dims(d, op, op == OP_DGRAD ? &ph[i] : nullptr, &M, &N, &K);
-    int best_c = heuristic_cfg(M, N, K);
+    gemm_dims(d, op, dtype, op == OP_DGRAD ? &ph[i] : nullptr, &M, &N, &K);
+    const int ncfg = cfg_count(dtype);
+    int best_c = heuristic_cfg(dtype, M, N, K);
     float best_t = 1e30f;
     auto time_cfg = [&](int c) -> float {
-      if (plan_ws(plan_with(c, M, N, K)) > ws_bytes) return 1e30f;
+      if (plan_ws(plan_with(dtype, c, M, N, K)) > ws_bytes) return 1e30f;
       rc = run_conv(d, op, dtype, A, B, C, 0, ws, ws_bytes, stream, c, op == OP_DGRAD ? i : -1);  // warm-up
       if (rc) return 1e30f;
       (void)hipEventRecord(e0, s);
@@ -935,16 +782,16 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
       return ms;
     };
     // pass 1: every tile with the planner's split-K factor
-    float tile_t[kNumCfgs];
-    for (int c = 0; c < kNumCfgs && !rc; ++c) tile_t[c] = time_cfg(c);
+    float tile_t[64];
+    for (int c = 0; c < ncfg && !rc; ++c) tile_t[c] = time_cfg(c);
     // pass 2: the three fastest tiles with other split-K factors
     for (int pick = 0; pick < 3 && !rc; ++pick) {
       int c = -1;
-      for (int k = 0; k < kNumCfgs; ++k)
+      for (int k = 0; k < ncfg; ++k)
         if (tile_t[k] < 1e29f && (c < 0 || tile_t[k] < tile_t[c])) c = k;
       if (c < 0) break;
       tile_t[c] = 1e30f;
-      const Plan dp = plan_with(c, M, N, K);
+      const Plan dp = plan_with(dtype, c, M, N, K);
       int prev = -1;
       for (int v : {1, dp.splits / 4, dp.splits / 2, dp.splits * 2}) {
         if (v < 1 || v == dp.splits || v == prev || v > 256 || v > dp.ktiles) continue;
@@ -955,7 +802,7 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
     }
     if (rc) break;
     std::lock_guard<std::mutex> lk(g_tune_mu);
-    g_tuned[tune_key(op, M, N, K, d)] = best_c;
+    g_tuned[tune_key(dtype, op, M, N, K, d)] = best_c;
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
@@ -967,9 +814,8 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
 using namespace jr;
 
 JR_API size_t jr_conv2d_workspace_size(const jr_conv_desc* d, int op, int dtype) {
-  (void)dtype;
-  if (!d || validate(d, op) != JR_OK) return 0;
-  return ws_bytes_for(d, op);
+  if (!d || validate(d, op, dtype) != JR_OK) return 0;
+  return ws_bytes_for(d, op, dtype);
 }
 
 JR_API int jr_conv2d_fwd(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y,
@@ -992,23 +838,23 @@ JR_API int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const vo
   return autotune(d, op, dtype, a, b, c, ws, ws_bytes, stream, 3);
 }
 
-JR_API int jr_conv2d_num_configs(void) { return kNumCfgs; }
+JR_API int jr_conv2d_num_configs(int dtype) { return dtype == JR_BF16 || dtype == JR_F32 ? cfg_count(dtype) : 0; }
 
 // Diagnostic: time `reps` launches of one FWD GEMM (no split-K) of tile
 // config `cfg` in variant dbg (0 normal, 1 no MFMA, 2 no DMA, 3 no LDS
 // reads); returns ms via *ms.  Results of variants 1-3 are garbage.
 JR_API int jr_conv2d_debug_time(const jr_conv_desc* d, int cfg, int dbg, const void* x, const void* w, void* y,
                                 int reps, float* ms, void* stream) {
-  int rc = validate(d, OP_FWD);
+  int rc = validate(d, OP_FWD, JR_F32);
   if (rc) return rc;
   if (cfg < 0 || cfg >= kNumCfgs || dbg < 0 || dbg > 3) return fail(JR_ERR_INVALID, "debug_time: bad cfg/dbg");
-  if (dbg > 0 && chan_pad(d->c_in) % kCfgs[cfg].bk != 0)
+  if (dbg > 0 && chan_pad(d->c_in, JR_F32) % kCfgs[cfg].bk != 0)
     return fail(JR_ERR_UNSUPPORTED, "debug_time: variants need c_in % BK == 0");
   ConvArgs a{};
-  fill_common(a, d);
+  fill_common(a, d, JR_F32);
   a.A = (const float*)x; a.B = (const float*)w; a.C = (float*)y;
   a.c_off = d->y_c_off; a.c_stride = d->y_c_stride;
-  Plan p = plan_for(d, OP_FWD, nullptr, cfg);
+  Plan p = plan_for(d, OP_FWD, JR_F32, nullptr, cfg);
   p.splits = 1; p.kt_per_split = p.ktiles;
   a.M = p.M; a.N = p.N; a.K = p.K; a.ktiles = p.ktiles; a.kt_per_split = p.kt_per_split; a.ntn = p.nt;
   hipStream_t s = as_stream(stream);
@@ -1033,10 +879,10 @@ JR_API int jr_conv2d_debug_time(const jr_conv_desc* d, int cfg, int dbg, const v
   return check_launch("debug_time");
 }
 
-JR_API int jr_conv2d_set_config(const jr_conv_desc* d, int op, int phase, int cfg) {
-  int rc = validate(d, op);
+JR_API int jr_conv2d_set_config(const jr_conv_desc* d, int op, int dtype, int phase, int cfg) {
+  int rc = validate(d, op, dtype);
   if (rc) return rc;
-  if (cfg < 0 || cfg_tile(cfg) >= kNumCfgs || cfg_splits(cfg) > 256)
+  if (cfg < 0 || cfg_tile(cfg) >= cfg_count(dtype) || cfg_splits(cfg) > 256)
     return fail(JR_ERR_INVALID, "conv set_config: bad config index");
   Phase ph[64];
   int nph = 1;
@@ -1045,19 +891,19 @@ JR_API int jr_conv2d_set_config(const jr_conv_desc* d, int op, int phase, int cf
     if (phase < 0 || phase >= nph) return fail(JR_ERR_INVALID, "conv set_config: bad phase");
   }
   int M, N, K;
-  gemm_dims(d, op, op == OP_DGRAD ? &ph[phase] : nullptr, &M, &N, &K);
+  gemm_dims(d, op, dtype, op == OP_DGRAD ? &ph[phase] : nullptr, &M, &N, &K);
   std::lock_guard<std::mutex> lk(g_tune_mu);
-  g_tuned[tune_key(op, M, N, K, d)] = cfg;
+  g_tuned[tune_key(dtype, op, M, N, K, d)] = cfg;
   return JR_OK;
 }
 
-JR_API int jr_conv2d_get_config(const jr_conv_desc* d, int op, int phase) {
-  if (!d || validate(d, op) != JR_OK) return -1;
+JR_API int jr_conv2d_get_config(const jr_conv_desc* d, int op, int dtype, int phase) {
+  if (!d || validate(d, op, dtype) != JR_OK) return -1;
   Phase ph[64];
   int nph = 1;
   if (op == OP_DGRAD) {
     dgrad_phases(d, ph, &nph);
     if (phase < 0 || phase >= nph) return -1;
   }
-  return plan_for(d, op, op == OP_DGRAD ? &ph[phase] : nullptr).cfg;
+  return plan_for(d, op, dtype, op == OP_DGRAD ? &ph[phase] : nullptr).cfg;
 }

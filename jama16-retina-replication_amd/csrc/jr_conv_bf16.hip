@@ -1,0 +1,424 @@
+// jr_conv_bf16.hip — the bf16 implicit-GEMM convolution (configs 3 and 5 of
+// BASELINE: bf16 MFMA training), v_mfma_f32_32x32x16_bf16 with fp32
+// accumulation.  Same GEMM mapping, phase decomposition, split-K and host
+// planning as the fp32 kernel in jr_conv.hip (which documents them); what
+// differs is the operand staging:
+//   * 16 B LDS-DMA pieces carry 8 bf16 channels, so channel radices are
+//     padded to 8 (conv1: c_in 3 -> 8, virtual zero channels);
+//   * every FWD / DGRAD operand is a KC image (k contiguous): FWD's filter is
+//     the transposed bf16 copy W^T [c_out][kh*kw*c8] that
+//     jr_conv_weights_bf16 writes, so B rows are k-linear; one ds_read_b128
+//     is exactly one MFMA operand (8 consecutive k of one row);
+//   * WGRAD's operands (x and dy, both contiguous along m / n) are MC images
+//     [BK][cols] read with ds_read_b64_tr_b16, the gfx950 transposing LDS
+//     read: per 16-lane group a 4 (k) x 16 (col) block arrives column-major,
+//     two reads give a lane its 8 k values.
+// Outputs: FWD / DGRAD write bf16 (fp32 accumulate, one rounding; split-K
+// slabs stay fp32 and the reduce rounds), WGRAD writes fp32 dW.
+#include "jr_conv_impl.h"
+
+namespace jr {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// ds_read_b64_tr_b16: lane 4q+p of each 16-lane group passes the address of
+// row q, columns 4p..4p+3 of the group's 4x16 block; lane i gets column i.
+__device__ __forceinline__ s16x4 lds_tr(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(const_cast<uint16_t*>(p)));
+}
+
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT>
+__global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
+  constexpr int WGN = 4 / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  static_assert(WM % 32 == 0 && WN % 32 == 0, "wave tile must be a multiple of 32x32");
+  constexpr int QPR = BK / 8;                 // 16 B quads per KC row
+  constexpr int RPI = 64 / QPR;               // KC rows per DMA instruction
+  constexpr int SWZ = 16 / QPR;               // rows sharing one swizzle value
+  constexpr int KSTEPS = BK / 16;             // MFMA k-steps per tile
+  constexpr bool MC = (OP == OP_WGRAD);       // both operands MC (else both KC)
+  constexpr int ASZ = BM * BK, BSZ = BN * BK;  // bf16 elements per image
+  constexpr int A_INSTR = ASZ / 512, B_INSTR = BSZ / 512;
+  constexpr int A_PW = (A_INSTR + 3) / 4, B_PW = (B_INSTR + 3) / 4;  // per wave
+  static_assert(ASZ % 512 == 0 && BSZ % 512 == 0, "tile must be whole DMA instructions");
+  static_assert(BK % 16 == 0 && QPR <= 8, "BK must be 16..64");
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[NBUF * (ASZ + BSZ)];
+
+  const uint16_t* __restrict__ gA = reinterpret_cast<const uint16_t*>(g.A);
+  const uint16_t* __restrict__ gB = reinterpret_cast<const uint16_t*>(g.B);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm0 = (wave / WGN) * WM;
+  const int wn0 = (wave % WGN) * WN;
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / g.ntn, nt = tile - mt * g.ntn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int kt0 = blockIdx.z * g.kt_per_split;
+  const int kt1 = min(g.ktiles, kt0 + g.kt_per_split);
+  const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
+  const int cred = OP == OP_FWD ? g.cp : g.cout;
+  // FWD/DGRAD: UT = wave-uniform tap (cred % BK == 0); WGRAD: UT = wo >= BK.
+  constexpr bool ut = UT && OP != OP_WGRAD;
+
+  // ---------------------------------------------------------------- A state
+  const uint16_t* a_ptr[A_PW];
+  int a_p0[A_PW], a_p1[A_PW], a_p2[A_PW];
+  int a_s0[A_PW], a_s1[A_PW], a_s2[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int j = wave + 4 * i;
+    a_ptr[i] = zp;
+    a_p0[i] = a_p1[i] = a_p2[i] = 0;
+    a_s0[i] = a_s1[i] = a_s2[i] = 0;
+    if (A_INSTR % 4 != 0 && j >= A_INSTR) continue;
+    if constexpr (!MC) {
+      const int row = j * RPI + lane / QPR;
+      const int q = (lane % QPR) ^ ((row / SWZ) % QPR);
+      const int m = m0 + row;
+      const int k = kt0 * BK + q * 8;
+      if constexpr (OP == OP_FWD) {
+        int pix = 0;
+        if (m < g.M) {
+          const int hw = g.ho * g.wo;
+          const int b = m / hw, rem = m - b * hw;
+          const int oh = rem / g.wo, ow = rem - oh * g.wo;
+          a_p0[i] = oh * g.sh - g.ph;
+          a_p1[i] = ow * g.sw - g.pw;
+          a_p2[i] = b * g.h * g.w;
+          pix = a_p2[i] + a_p0[i] * g.w + a_p1[i];
+        } else {
+          a_p0[i] = -(1 << 28);
+        }
+        a_ptr[i] = gA + ((long long)pix * g.xs + g.xo + q * 8);
+        const int rc = k / g.cp;
+        a_s2[i] = k - rc * g.cp;
+        a_s0[i] = rc / g.kw;
+        a_s1[i] = rc - a_s0[i] * g.kw;
+      } else {  // DGRAD
+        int pix = 0;
+        if (m < g.M) {
+          const int hw = g.hc * g.wc;
+          const int b = m / hw, rem = m - b * hw;
+          const int u = rem / g.wc, v = rem - u * g.wc;
+          a_p0[i] = u + g.ey;
+          a_p1[i] = v + g.ex;
+          a_p2[i] = b * g.ho * g.wo;
+          pix = a_p2[i] + a_p0[i] * g.wo + a_p1[i];
+        } else {
+          a_p0[i] = -(1 << 28);
+        }
+        a_ptr[i] = gA + ((long long)pix * g.ys + g.yo + q * 8);
+        const int ab = k / g.cout;
+        a_s2[i] = k - ab * g.cout;
+        a_s0[i] = ab / g.nb;
+        a_s1[i] = ab - a_s0[i] * g.nb;
+      }
+    } else {  // WGRAD MC: m = (r,c,ci) fixed per slot (8 channels), k = pixel
+      const int flat = j * 512 + lane * 8;
+      const int krow = flat / BM, col = flat - krow * BM;
+      const int m = m0 + col;
+      if (m < g.M) {
+        const int rc = m / g.cp, ci = m - rc * g.cp;
+        const int r = rc / g.kw, c = rc - r * g.kw;
+        a_p0[i] = r - g.ph;
+        a_p1[i] = c - g.pw;
+        a_p2[i] = ci;
+      } else {
+        a_p0[i] = -(1 << 28);
+      }
+      const int pix = kt0 * BK + krow;
+      const int hw = g.ho * g.wo;
+      a_s0[i] = pix / hw;
+      const int rem = pix - a_s0[i] * hw;
+      a_s1[i] = rem / g.wo;
+      a_s2[i] = rem - a_s1[i] * g.wo;
+    }
+  }
+  // ---------------------------------------------------------------- B state
+  const uint16_t* b_ptr[B_PW];
+  int b_p0[B_PW], b_s0[B_PW], b_s1[B_PW], b_s2[B_PW];
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int j = wave + 4 * i;
+    b_ptr[i] = zp;
+    b_p0[i] = b_s0[i] = b_s1[i] = b_s2[i] = 0;
+    if (B_INSTR % 4 != 0 && j >= B_INSTR) continue;
+    if constexpr (!MC) {
+      const int row = j * RPI + lane / QPR;
+      const int q = (lane % QPR) ^ ((row / SWZ) % QPR);
+      const int nn = n0 + row;
+      b_p0[i] = nn < g.N ? nn : -1;
+      const int k = kt0 * BK + q * 8;
+      if constexpr (OP == OP_FWD) {   // W^T [N][K]: k-linear rows
+        b_s0[i] = k;
+        b_ptr[i] = gB + ((long long)(nn < g.N ? nn : 0) * g.K + k);
+      } else {                        // DGRAD: W[(r,c)][ci][co], rows = ci, k = (a, bb, co)
+        b_ptr[i] = gB + ((long long)(nn < g.N ? nn : 0) * g.cout + q * 8);
+        const int ab = k / g.cout;
+        b_s2[i] = k - ab * g.cout;
+        b_s0[i] = ab / g.nb;
+        b_s1[i] = ab - b_s0[i] * g.nb;
+      }
+    } else {  // WGRAD MC: dy rows = k (pixels), cols = n
+      const int flat = j * 512 + lane * 8;
+      const int krow = flat / BN, col = flat - krow * BN;
+      b_p0[i] = (n0 + col < g.N) ? n0 + col : -1;
+      b_s0[i] = kt0 * BK + krow;
+      b_ptr[i] = gB + ((long long)b_s0[i] * g.ys + g.yo + n0 + col);
+    }
+  }
+  int t_r = 0, t_c = 0, t_ch = 0;
+  if constexpr (ut) {
+    const int k = kt0 * BK;
+    const int rc = k / cred;
+    t_ch = k - rc * cred;
+    t_r = rc / (OP == OP_FWD ? g.kw : g.nb);
+    t_c = rc - t_r * (OP == OP_FWD ? g.kw : g.nb);
+  }
+
+  const bool a_multi = !MC ? (cred < BK) : (!UT && g.wo < BK);
+  const bool b_multi = (OP == OP_DGRAD) ? (g.cout < BK) : false;
+
+  // DMA of one operand piece of tile kt (d < A_PW: A slot d, else B slot).
+  auto issue_piece = [&](int kt, int d, uint16_t* __restrict__ As, uint16_t* __restrict__ Bs) {
+    if (d < A_PW) {
+      const int i = d;
+      const int j = wave + 4 * i;
+      if (A_INSTR % 4 != 0 && j >= A_INSTR) return;
+      if constexpr (!MC && ut) {
+        long long off;
+        int dr, dc;
+        if constexpr (OP == OP_FWD) {
+          off = (long long)(t_r * g.w + t_c) * g.xs + t_ch;
+          dr = t_r; dc = t_c;
+        } else {
+          off = -(long long)(t_r * g.wo + t_c) * g.ys + t_ch;
+          dr = -t_r; dc = -t_c;
+        }
+        const int hmax = OP == OP_FWD ? g.h : g.ho, wmax = OP == OP_FWD ? g.w : g.wo;
+        const bool ok = (unsigned)(a_p0[i] + dr) < (unsigned)hmax && (unsigned)(a_p1[i] + dc) < (unsigned)wmax;
+        dma16(ok ? a_ptr[i] + off : zp, As + j * 512);
+      } else {
+        const uint16_t* src = zp;
+        if constexpr (OP == OP_FWD) {
+          const int hi = a_p0[i] + a_s0[i], wi = a_p1[i] + a_s1[i];
+          const bool ok = (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w && a_s0[i] < g.kh;
+          const uint16_t* p = gA + ((a_p2[i] + hi * g.w + wi) * g.xs + g.xo + a_s2[i]);
+          src = ok ? p : zp;
+          adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cp, g.kw, a_multi);
+        } else if constexpr (OP == OP_DGRAD) {
+          const int oh = a_p0[i] - a_s0[i], ow = a_p1[i] - a_s1[i];
+          const bool ok = (unsigned)oh < (unsigned)g.ho && (unsigned)ow < (unsigned)g.wo && a_s0[i] < g.na;
+          const uint16_t* p = gA + ((a_p2[i] + oh * g.wo + ow) * g.ys + g.yo + a_s2[i]);
+          src = ok ? p : zp;
+          adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cout, g.nb, a_multi);
+        } else {  // WGRAD
+          const int hi = a_s1[i] * g.sh + a_p0[i], wi = a_s2[i] * g.sw + a_p1[i];
+          const bool ok = a_s0[i] < g.n && (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w;
+          const uint16_t* p = gA + (((a_s0[i] * g.h + hi) * g.w + wi) * g.xs + g.xo + a_p2[i]);
+          src = ok ? p : zp;
+          adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.wo, g.ho, a_multi);
+        }
+        dma16(src, As + j * 512);
+      }
+      return;
+    }
+    const int i = d - A_PW;
+    const int j = wave + 4 * i;
+    if (B_INSTR % 4 != 0 && j >= B_INSTR) return;
+    if constexpr (OP == OP_FWD) {
+      const int k = b_s0[i] + (kt - kt0) * BK;
+      const bool ok = b_p0[i] >= 0 && k < g.K;
+      dma16(ok ? b_ptr[i] + (kt - kt0) * BK : zp, Bs + j * 512);
+    } else if constexpr (OP == OP_DGRAD) {
+      if constexpr (ut) {
+        const long long off = (long long)((g.r0 + g.sh * t_r) * g.kw + (g.c0 + g.sw * t_c)) * g.cin * g.cout + t_ch;
+        dma16(b_p0[i] >= 0 ? b_ptr[i] + off : zp, Bs + j * 512);
+      } else {
+        const bool ok = b_p0[i] >= 0 && b_s0[i] < g.na;
+        const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
+        const uint16_t* p = gB + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
+        dma16(ok ? p : zp, Bs + j * 512);
+        adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
+      }
+    } else {  // WGRAD
+      const int k = b_s0[i] + (kt - kt0) * BK;
+      const bool ok = b_p0[i] >= 0 && k < g.K;
+      dma16(ok ? b_ptr[i] + (long long)(kt - kt0) * BK * g.ys : zp, Bs + j * 512);
+    }
+  };
+  auto advance = [&]() {
+    if constexpr (ut) {
+      t_ch += BK;
+      const bool w1 = t_ch == cred;
+      t_ch = w1 ? 0 : t_ch;
+      t_c += w1 ? 1 : 0;
+      const bool w2 = t_c == (OP == OP_FWD ? g.kw : g.nb);
+      t_c = w2 ? 0 : t_c;
+      t_r += w2 ? 1 : 0;
+    }
+  };
+  constexpr int NPIECE = A_PW + B_PW;
+  auto issue = [&](int kt, uint16_t* __restrict__ As, uint16_t* __restrict__ Bs) {
+#pragma unroll
+    for (int d = 0; d < NPIECE; ++d) issue_piece(kt, d, As, Bs);
+    advance();
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int l31 = lane & 31, lh = lane >> 5;
+  // transposed-read lane roles (MC): 16-lane group g16 = lh*2 + hb
+  const int hb = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+  constexpr int per_tile = A_INSTR / 4 + B_INSTR / 4;
+
+  auto step = [&](int kt, auto do_issue, const uint16_t* __restrict__ As, const uint16_t* __restrict__ Bs,
+                  uint16_t* __restrict__ wA, uint16_t* __restrict__ wB) {
+    constexpr bool DO_ISSUE = decltype(do_issue)::value;
+    bf16x8 af[TM][KSTEPS], bfr[TN][KSTEPS];
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if constexpr (!MC) {
+          const int row = wm0 + i * 32 + l31;
+          const int f = (row / SWZ) % QPR;
+          af[i][s] = *reinterpret_cast<const bf16x8*>(As + row * BK + (((2 * s + lh) ^ f) * 8));
+        } else {
+          const uint16_t* p = As + (16 * s + 8 * lh + tq) * BM + wm0 + i * 32 + 16 * hb + 4 * tp;
+          const s16x4 lo = lds_tr(p), hi = lds_tr(p + 4 * BM);
+          af[i][s] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (!MC) {
+          const int row = wn0 + j * 32 + l31;
+          const int f = (row / SWZ) % QPR;
+          bfr[j][s] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + (((2 * s + lh) ^ f) * 8));
+        } else {
+          const uint16_t* p = Bs + (16 * s + 8 * lh + tq) * BN + wn0 + j * 32 + 16 * hb + 4 * tp;
+          const s16x4 lo = lds_tr(p), hi = lds_tr(p + 4 * BN);
+          bfr[j][s] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      }
+    }
+    // MFMAs of k-step s, then this step's share of the DMA pieces of tile
+    // kt+NBUF-1 (the LDS-DMA intrinsic is a scheduling boundary for hipcc)
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+      if constexpr (DO_ISSUE) {
+#pragma unroll
+        for (int d = s * NPIECE / KSTEPS; d < (s + 1) * NPIECE / KSTEPS; ++d) issue_piece(kt + NBUF - 1, d, wA, wB);
+      }
+    }
+    if constexpr (DO_ISSUE) advance();
+  };
+  auto buf_a = [&](int b) { return smem + b * (ASZ + BSZ); };
+  auto buf_b = [&](int b) { return smem + b * (ASZ + BSZ) + ASZ; };
+
+  if (kt0 < kt1) {
+#pragma unroll
+    for (int p = 0; p < NBUF - 1; ++p)
+      if (kt0 + p < kt1) issue(kt0 + p, buf_a(p), buf_b(p));
+    wait_vmcnt(per_tile * min(NBUF - 2, kt1 - kt0 - 1));
+    __builtin_amdgcn_s_barrier();
+    int cur = 0;
+    int kt = kt0;
+    for (; kt < kt1 - (NBUF - 1); ++kt) {
+      const int nxt = cur == 0 ? NBUF - 1 : cur - 1;
+      step(kt, std::true_type{}, buf_a(cur), buf_b(cur), buf_a(nxt), buf_b(nxt));
+      __builtin_amdgcn_sched_barrier(0);
+      wait_vmcnt(per_tile * (NBUF - 2));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      cur = cur + 1 == NBUF ? 0 : cur + 1;
+    }
+    for (; kt < kt1; ++kt) {
+      step(kt, std::false_type{}, buf_a(cur), buf_b(cur), nullptr, nullptr);
+      __builtin_amdgcn_sched_barrier(0);
+      wait_vmcnt(per_tile * max(0, min(NBUF - 2, kt1 - kt - 2)));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      cur = cur + 1 == NBUF ? 0 : cur + 1;
+    }
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const bool split = gridDim.z > 1;
+  const int rbase = 4 * lh;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
+      if (m >= g.M) continue;
+      const long long base = split ? (long long)m * g.N : out_row<OP>(g, m);
+      if (base < 0) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn0 + j * 32 + l31;
+        if (n >= g.N) continue;
+        if (split) {
+          g.C[(long long)blockIdx.z * g.slab_elems + base + n] = acc[i][j][r];
+        } else if constexpr (OP == OP_WGRAD) {
+          g.C[base + n] = acc[i][j][r];
+        } else {
+          uint16_t* p = reinterpret_cast<uint16_t*>(g.C) + base + n;
+          float v = acc[i][j][r];
+          if (g.accumulate) v += bf2f(*p);
+          *p = f2bf(v);
+        }
+      }
+    }
+  }
+}
+
+template <int OP, int C>
+static void launch_tile(bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
+  constexpr TileCfg t = kCfgsBf16[C];
+  if (fast)
+    hipLaunchKernelGGL((k_conv_bf16<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_conv_bf16<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false>), grid, dim3(256), 0, s, a);
+}
+
+template <int OP>
+static void launch_op_bf16(int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
+  static_assert(kNumCfgsBf16 == 8, "keep the switch in sync with kCfgsBf16");
+  switch (tile) {
+    case 0: launch_tile<OP, 0>(fast, a, grid, s); break;
+    case 1: launch_tile<OP, 1>(fast, a, grid, s); break;
+    case 2: launch_tile<OP, 2>(fast, a, grid, s); break;
+    case 3: launch_tile<OP, 3>(fast, a, grid, s); break;
+    case 4: launch_tile<OP, 4>(fast, a, grid, s); break;
+    case 5: launch_tile<OP, 5>(fast, a, grid, s); break;
+    case 6: launch_tile<OP, 6>(fast, a, grid, s); break;
+    default: launch_tile<OP, 7>(fast, a, grid, s); break;
+  }
+}
+
+void launch_conv_bf16(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
+  if (op == OP_FWD) launch_op_bf16<OP_FWD>(tile, fast, a, grid, s);
+  else if (op == OP_DGRAD) launch_op_bf16<OP_DGRAD>(tile, fast, a, grid, s);
+  else launch_op_bf16<OP_WGRAD>(tile, fast, a, grid, s);
+}
+
+}  // namespace jr

@@ -167,6 +167,80 @@ JR_API int jr_adam_update(float* w, const float* grad, float* m, float* v, int64
   return check_launch("adam");
 }
 
+// ---------------------------------------------------------------- bf16 filters
+// One block = one 32 (c_in) x 32 (c_out) tile of one tap of one layer:
+// coalesced read along c_out, bf16 HWIO write along c_out, transpose through
+// LDS, bf16 W^T write along c_in (zero channels up to c8).
+static __device__ __forceinline__ int wprep_tiles(int kh, int kw, int cin, int cout) {
+  return kh * kw * ((((cin + 7) / 8 * 8) + 31) / 32) * ((cout + 31) / 32);
+}
+
+template <bool SINGLE>
+__global__ void __launch_bounds__(256) k_wprep(const jr_wprep* __restrict__ table, jr_wprep one, int nl,
+                                               const float* __restrict__ src, uint16_t* hwio, uint16_t* wt) {
+  __shared__ float t[32][33];
+  const int tile = blockIdx.x;
+  jr_wprep L;
+  if constexpr (SINGLE) {
+    L = one;
+  } else {   // last layer whose tile_start <= tile
+    int lo = 0, hi = nl - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (table[mid].tile_start <= tile) lo = mid; else hi = mid - 1;
+    }
+    L = table[lo];
+  }
+  const int c8 = (L.c_in + 7) / 8 * 8;
+  const int cit = (c8 + 31) / 32, cot = (L.c_out + 31) / 32;
+  const int local = tile - (SINGLE ? 0 : L.tile_start);
+  const int tap = local / (cit * cot), rem = local - tap * (cit * cot);
+  const int ci0 = (rem / cot) * 32, co0 = (rem % cot) * 32;
+  const float* s = src + L.src_off;
+  for (int e = threadIdx.x; e < 1024; e += 256) {
+    const int ci = ci0 + (e >> 5), co = co0 + (e & 31);
+    float v = 0.f;
+    if (ci < L.c_in && co < L.c_out) {
+      const int64_t idx = ((int64_t)tap * L.c_in + ci) * L.c_out + co;
+      v = s[idx];
+      if (hwio) hwio[L.hwio_off + idx] = f2bf(v);
+    }
+    t[e >> 5][e & 31] = v;
+  }
+  __syncthreads();
+  if (!wt) return;
+  const int64_t K = (int64_t)L.kh * L.kw * c8;
+  for (int e = threadIdx.x; e < 1024; e += 256) {
+    const int co = co0 + (e >> 5), ci = ci0 + (e & 31);
+    if (co < L.c_out && ci < c8) wt[L.wt_off + co * K + (int64_t)tap * c8 + ci] = f2bf(t[e & 31][e >> 5]);
+  }
+}
+
+JR_API int32_t jr_conv_weights_bf16_tiles(int32_t kh, int32_t kw, int32_t c_in, int32_t c_out) {
+  if (kh <= 0 || kw <= 0 || c_in <= 0 || c_out <= 0) return 0;
+  return kh * kw * ((((c_in + 7) / 8 * 8) + 31) / 32) * ((c_out + 31) / 32);
+}
+
+JR_API int jr_conv_weights_bf16(const float* w, int32_t kh, int32_t kw, int32_t c_in, int32_t c_out, void* w_hwio,
+                                void* w_t, void* stream) {
+  const int tiles = jr_conv_weights_bf16_tiles(kh, kw, c_in, c_out);
+  if (!w || tiles <= 0) return fail(JR_ERR_INVALID, "conv_weights_bf16: bad arguments");
+  jr_wprep one{0, 0, 0, kh, kw, c_in, c_out, 0, 0};
+  hipLaunchKernelGGL(k_wprep<true>, dim3(tiles), dim3(256), 0, as_stream(stream), (const jr_wprep*)nullptr, one, 1,
+                     w, (uint16_t*)w_hwio, (uint16_t*)w_t);
+  return check_launch("conv_weights_bf16");
+}
+
+JR_API int jr_conv_weights_bf16_multi(const jr_wprep* layers, int32_t n_layers, int32_t total_tiles, const float* src,
+                                      void* hwio, void* wt, void* stream) {
+  if (!layers || !src || n_layers <= 0 || total_tiles < 0) return fail(JR_ERR_INVALID, "conv_weights_bf16_multi: bad arguments");
+  if (total_tiles == 0) return JR_OK;
+  jr_wprep none{};
+  hipLaunchKernelGGL(k_wprep<false>, dim3(total_tiles), dim3(256), 0, as_stream(stream), layers, none, n_layers, src,
+                     (uint16_t*)hwio, (uint16_t*)wt);
+  return check_launch("conv_weights_bf16_multi");
+}
+
 JR_API int jr_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream) {
   if (!src || !dst || n < 0) return fail(JR_ERR_INVALID, "cast: bad arguments");
   if (n == 0) return JR_OK;

@@ -35,6 +35,13 @@ class ConvDesc(Structure):
         "ho", "wo", "x_c_off", "x_c_stride", "y_c_off", "y_c_stride")]
 
 
+class WPrep(Structure):
+    """include/jr.h: struct jr_wprep (one layer of jr_conv_weights_bf16_multi)."""
+    _fields_ = [("src_off", c_int64), ("hwio_off", c_int64), ("wt_off", c_int64), ("kh", c_int32),
+                ("kw", c_int32), ("c_in", c_int32), ("c_out", c_int32), ("tile_start", c_int32),
+                ("reserved", c_int32)]
+
+
 class PoolDesc(Structure):
     _fields_ = [(n, c_int32) for n in (
         "n", "h", "w", "c", "ho", "wo", "x_c_off", "x_c_stride", "y_c_off", "y_c_stride")]
@@ -54,9 +61,14 @@ _SIGS = {
                                      c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_autotune": (c_int, [POINTER(ConvDesc), c_int, c_int, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_size_t, c_void_p]),
-    "jr_conv2d_get_config": (c_int, [POINTER(ConvDesc), c_int, c_int]),
-    "jr_conv2d_set_config": (c_int, [POINTER(ConvDesc), c_int, c_int, c_int]),
-    "jr_conv2d_num_configs": (c_int, []),
+    "jr_conv2d_get_config": (c_int, [POINTER(ConvDesc), c_int, c_int, c_int]),
+    "jr_conv2d_set_config": (c_int, [POINTER(ConvDesc), c_int, c_int, c_int, c_int]),
+    "jr_conv2d_num_configs": (c_int, [c_int]),
+    "jr_conv_weights_bf16_tiles": (c_int32, [c_int32, c_int32, c_int32, c_int32]),
+    "jr_conv_weights_bf16": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                     c_void_p]),
+    "jr_conv_weights_bf16_multi": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                           c_void_p]),
     "jr_bn_workspace_size": (c_size_t, [c_int64, c_int32]),
     "jr_bn_stats": (c_int, [c_int, c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
                             c_void_p, c_size_t, c_void_p]),
@@ -133,7 +145,8 @@ def call(name: str, *args) -> int:
     lib = load()
     rc = getattr(lib, name)(*args)
     if isinstance(rc, int) and name not in ("jr_conv2d_workspace_size", "jr_bn_workspace_size",
-                                            "jr_conv2d_get_config", "jr_conv2d_num_configs"):
+                                            "jr_conv2d_get_config", "jr_conv2d_num_configs",
+                                            "jr_conv_weights_bf16_tiles"):
         check(name, rc)
     return rc
 

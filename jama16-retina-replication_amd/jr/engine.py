@@ -152,9 +152,9 @@ class Engine:
         out = {}
         for n in self.g.convs:
             d = self._conv_desc(n, self.batch)
-            f = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_FWD, 0)
-            wg = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, 0)
-            dg = [self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, p)
+            f = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_FWD, self.dt, 0)
+            wg = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, self.dt, 0)
+            dg = [self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.dt, p)
                   for p in range(n.stride * n.stride)]
             out[n.name] = (f, wg, dg)
         return out

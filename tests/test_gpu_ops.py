@@ -144,10 +144,10 @@ def test_conv_every_tile_config(case):
     wsb = max(L.jr_conv2d_workspace_size(ctypes.byref(d), op, 0) for op in range(3))
     wsb += 3 * 4 * max(n * ho * wo * cout, kh * kw * cs * cout, n * h * w * cs)   # forced splits of 3
     ws = torch.zeros(wsb // 4 + 4, device="cuda")
-    cfgs = [t | (sp << 8) for t in range(L.jr_conv2d_num_configs()) for sp in (0, 1, 3)]  # forced split-K
+    cfgs = [t | (sp << 8) for t in range(L.jr_conv2d_num_configs(0)) for sp in (0, 1, 3)]  # forced split-K
     for cfg in cfgs:
-        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, 0, cfg))
-        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 2, 0, cfg))
+        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, 0, 0, cfg))
+        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 2, 0, 0, cfg))
         Y = torch.zeros(ref.size, device="cuda")
         ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), 0, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
                                          ws.data_ptr(), wsb, None))
@@ -158,7 +158,7 @@ def test_conv_every_tile_config(case):
         assert relerr(host(DW).reshape(wt.shape), ref_dw) < 1e-5, cfg
         if ref_dx is not None:
             for ph in range(s * s):
-                ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 1, ph, cfg))
+                ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 1, 0, ph, cfg))
             DX = torch.zeros(x.size, device="cuda")
             ffi.check("dgrad", L.jr_conv2d_bwd_data(ctypes.byref(d), 0, DY.data_ptr(), W.data_ptr(), DX.data_ptr(),
                                                     0, ws.data_ptr(), wsb, None))
