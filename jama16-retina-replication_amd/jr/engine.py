@@ -43,8 +43,6 @@ class Engine:
                  autotune: bool = True):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
-        if dtype != "f32":
-            raise NotImplementedError("bf16 path: kernels land in a later round")
         if not torch.cuda.is_available():
             raise RuntimeError("jr.Engine needs a ROCm GPU (libjr has no CPU path)")
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
@@ -79,12 +77,18 @@ class Engine:
     def _alloc(self) -> None:
         g, B = self.g, self.batch
         fl = torch.float32
-        # the image buffer is kept 4 channels wide (zero 4th channel): conv1's
-        # c_in = 3 runs on libjr's virtual channel padding
-        self.in_stride = (g.bufs[g.input_buf].c + 3) // 4 * 4
-        self.acts = [self._t(B * b.h * b.w * (self.in_stride if b.id == g.input_buf else b.c), fl)
+        # activation dtype: fp32, or bf16 (parameters, gradients, momentum,
+        # BN statistics and the head stay fp32 master copies either way)
+        at = torch.bfloat16 if self.dt == _ffi.JR_BF16 else fl
+        self.act_dtype = at
+        # the image buffer is kept one 16 B DMA piece wide per pixel (4 fp32 /
+        # 8 bf16 channels, zeros past c = 3): conv1's c_in = 3 runs on libjr's
+        # virtual channel padding
+        q = 8 if self.dt == _ffi.JR_BF16 else 4
+        self.in_stride = (g.bufs[g.input_buf].c + q - 1) // q * q
+        self.acts = [self._t(B * b.h * b.w * (self.in_stride if b.id == g.input_buf else b.c), at)
                      for b in g.bufs]
-        self.raw = {n.idx: self._t(B * n.ho * n.wo * n.cout) for n in g.convs}
+        self.raw = {n.idx: self._t(B * n.ho * n.wo * n.cout, at) for n in g.convs}
         self.stats = self._t(2 * sum(n.cout for n in g.convs))
         self.mean, self.invstd = {}, {}
         off = 0
@@ -106,10 +110,12 @@ class Engine:
         if self.train_mode:
             self.grads = self._t(self.nparam)
             self.accum = self._t(self.nparam)
-            self.dacts = [self._t(B * b.h * b.w * b.c) if b.id != g.input_buf else None
+            self.dacts = [self._t(B * b.h * b.w * b.c, at) if b.id != g.input_buf else None
                           for b in g.bufs]
-            self.draw = self._t(max(B * n.ho * n.wo * n.cout for n in g.convs))
+            self.draw = self._t(max(B * n.ho * n.wo * n.cout for n in g.convs), at)
             self.dfeat = self._t(B * feat_c)
+        if self.dt == _ffi.JR_BF16:
+            self._alloc_bf16_filters()
         ws = 0
         for n in g.convs:
             d = self._conv_desc(n, B)
@@ -120,6 +126,46 @@ class Engine:
         self.ws_bytes = int(ws)
         self.ws = self._t((self.ws_bytes + 15) // 4 + 4)
 
+    def _alloc_bf16_filters(self) -> None:
+        """bf16 operand copies of every conv kernel, refreshed from the fp32
+        master parameters by ONE jr_conv_weights_bf16_multi launch at the
+        start of each forward: HWIO (bwd_data) and W^T [co][kh][kw][c8] (fwd)."""
+        L = self.lib
+        layers, tiles = [], 0
+        self.wb_hwio_off, self.wb_t_off = {}, {}
+        ho = to = 0
+        for n in self.g.convs:
+            src, _ = self.poffs[f"{n.name}/kernel"]
+            c8 = (n.cin + 7) // 8 * 8
+            layers.append(_ffi.WPrep(src, ho, to, n.kh, n.kw, n.cin, n.cout, tiles, 0))
+            self.wb_hwio_off[n.idx], self.wb_t_off[n.idx] = ho, to
+            tiles += L.jr_conv_weights_bf16_tiles(n.kh, n.kw, n.cin, n.cout)
+            # 16 B-aligned starts (8 bf16)
+            ho += (n.kh * n.kw * n.cin * n.cout + 7) // 8 * 8
+            to += n.cout * n.kh * n.kw * c8
+        arr = (_ffi.WPrep * len(layers))(*layers)
+        self.wprep_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
+        self.wprep_layers, self.wprep_tiles = len(layers), tiles
+        self.w_hwio = self._t(ho, torch.bfloat16)
+        self.w_t = self._t(to, torch.bfloat16)
+
+    def _wprep_call(self):
+        return (self.lib.jr_conv_weights_bf16_multi,
+                (self.wprep_table.data_ptr(), self.wprep_layers, self.wprep_tiles, self.params.data_ptr(),
+                 self.w_hwio.data_ptr(), self.w_t.data_ptr(), self._s), "wprep_bf16")
+
+    def _wf(self, n: ConvNode) -> int:
+        """Filter operand of conv fwd: fp32 HWIO master, or the bf16 W^T copy."""
+        if self.dt == _ffi.JR_BF16:
+            return self.w_t.data_ptr() + 2 * self.wb_t_off[n.idx]
+        return self._p(f"{n.name}/kernel")
+
+    def _wd(self, n: ConvNode) -> int:
+        """Filter operand of conv bwd_data: fp32 HWIO master, or its bf16 copy."""
+        if self.dt == _ffi.JR_BF16:
+            return self.w_hwio.data_ptr() + 2 * self.wb_hwio_off[n.idx]
+        return self._p(f"{n.name}/kernel")
+
     def autotune(self) -> None:
         """jr_conv2d_autotune every conv op of the planned batch (cudnnFind
         style: times each tile configuration on this engine's own buffers and
@@ -128,10 +174,13 @@ class Engine:
         L, B = self.lib, self.batch
         ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
         s = self._s
+        if self.dt == _ffi.JR_BF16:
+            fn, args, name = self._wprep_call()
+            _ffi.check(name, fn(*args))
         for n in self.g.convs:
             d = self._conv_desc(n, B)
             x = self.acts[n.x].data_ptr()
-            w = self._p(f"{n.name}/kernel")
+            w = self._wf(n)
             _ffi.check("autotune fwd", L.jr_conv2d_autotune(ctypes.byref(d), _ffi.JR_CONV_FWD, self.dt, x, w,
                                                              self.raw[n.idx].data_ptr(), ws, wsb, s))
             if not self.train_mode:
@@ -141,7 +190,7 @@ class Engine:
                 self._gp(f"{n.name}/kernel"), ws, wsb, s))
             if n.x != self.g.input_buf:
                 _ffi.check("autotune dgrad", L.jr_conv2d_autotune(
-                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.dt, self.draw.data_ptr(), w,
+                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.dt, self.draw.data_ptr(), self._wd(n),
                     self.dacts[n.x].data_ptr(), ws, wsb, s))
         self.synchronize()
         if self.train_mode:
@@ -203,13 +252,15 @@ class Engine:
         keep = []  # keep ctypes structs alive
         fwd, bwd, opt = [], [], []
         A = lambda bid: self.acts[bid].data_ptr()  # noqa: E731
+        if dt == _ffi.JR_BF16:
+            fwd.append(self._wprep_call())
         for i, n in enumerate(g.nodes):
             if n.kind == "conv":
                 d = self._conv_desc(n, B)
                 keep.append(d)
                 M = B * n.ho * n.wo
                 yb = g.bufs[n.y.buf]
-                fwd.append((L.jr_conv2d_fwd, (ctypes.byref(d), dt, A(n.x), self._p(f"{n.name}/kernel"),
+                fwd.append((L.jr_conv2d_fwd, (ctypes.byref(d), dt, A(n.x), self._wf(n),
                                               self.raw[n.idx].data_ptr(), ws, wsb, s), "conv_fwd"))
                 fwd.append((L.jr_bn_stats, (dt, self.raw[n.idx].data_ptr(), M, n.cout, BN_EPS,
                                             self.mean[n.idx].data_ptr(), self.invstd[n.idx].data_ptr(),
@@ -263,7 +314,7 @@ class Engine:
                                                          self._gp(f"{n.name}/kernel"), ws, wsb, s), "conv_wgrad"))
                     if n.x != g.input_buf:
                         bwd.append((L.jr_conv2d_bwd_data, (ctypes.byref(d), dt, self.draw.data_ptr(),
-                                                           self._p(f"{n.name}/kernel"), D(n.x), acc, ws, wsb, s),
+                                                           self._wd(n), D(n.x), acc, ws, wsb, s),
                                     "conv_dgrad"))
                         written.add(n.x)
                     bwd.append(("param_ready", self.poffs[f"{n.name}/kernel"][0], "hook"))
@@ -326,7 +377,7 @@ class Engine:
             else:
                 dst = self.acts[self.g.input_buf][:pixels * self.in_stride].view(pixels, self.in_stride)
                 dst[:, ib.c:].zero_()
-                dst[:, :ib.c].copy_(x.to(torch.float32).reshape(pixels, ib.c), non_blocking=True)
+                dst[:, :ib.c].copy_(x.to(torch.float32).reshape(pixels, ib.c).to(self.device, non_blocking=True))
             if labels is not None:
                 y = torch.as_tensor(labels, dtype=torch.float32).reshape(-1)
                 if y.numel() != B * self.units:

@@ -10,7 +10,8 @@ from oracle.inception_ref import InceptionV3Ref
 
 res = int(sys.argv[1]) if len(sys.argv) > 1 else 107
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-eng = Engine(B, res, res, seed=1)
+dtype = sys.argv[3] if len(sys.argv) > 3 else "f32"
+eng = Engine(B, res, res, seed=1, dtype=dtype)
 imgs = synth.fundus_batch(0, B, res)
 y = synth.labels(0, B)
 eng.set_batch(imgs, y)
@@ -21,8 +22,8 @@ ref32 = InceptionV3Ref(unflatten(eng.g, eng.params_numpy()), torch.float32)
 ref32.record = []
 ref32.train_step(imgs.astype(np.float32) * np.float32(1 / 255), y, {})
 eng.forward(); eng.backward(); eng.synchronize()
-acts = [a.cpu().numpy() for a in eng.acts]
-dacts = [None if d is None else d.cpu().numpy() for d in eng.dacts]
+acts = [a.float().cpu().numpy() for a in eng.acts]
+dacts = [None if d is None else d.float().cpu().numpy() for d in eng.dacts]
 for n, yo, y32 in zip(eng.g.convs, ref.record, ref32.record):
     bf = eng.g.bufs[n.y.buf]
     a = acts[n.y.buf].reshape(B, bf.h, bf.w, bf.c)[..., n.y.c_off:n.y.c_off + n.cout]
