@@ -12,14 +12,20 @@
 //         dbeta = sum dy'
 //         dx = invstd * (dy' - mean(dy') - xhat * mean(dy' * xhat))
 //
+// All passes are HBM-streaming: every thread moves one 16-byte vector per
+// row (4 fp32 or 8 bf16 channels) and keeps several rows in flight.
 // Reductions are per-chunk partial sums in fp64 combined in a fixed chunk
-// order (deterministic, no atomics).  All passes are HBM-streaming kernels
-// with 16-byte (fp32x4) accesses along the channel axis.
+// order (deterministic, no atomics).
 #include "jr_common.h"
+
+#include <algorithm>
 
 namespace jr {
 
-constexpr int kMaxChunks = 1024;
+constexpr int kMaxChunks = 1024;  // partial sums per channel (finalize reads them)
+// rows in flight per thread in the reductions (16 B per row and operand)
+template <int MODE> constexpr int red_rows() { return MODE == 0 ? 16 : 8; }
+constexpr int kAppUnroll = 4;     // rows per thread in the elementwise passes
 
 // Same rounding in fwd and bwd so the ReLU mask is bit-identical.
 __device__ __forceinline__ float bn_xhat(float x, float mean, float invstd) {
@@ -29,119 +35,161 @@ __device__ __forceinline__ float bn_pre(float x, float mean, float invstd, float
   return __fadd_rn(bn_xhat(x, mean, invstd), beta);
 }
 
-template <typename T> struct V4;
-template <> struct V4<float> {
-  __device__ static float4 ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
-  __device__ static void st(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
-};
-template <> struct V4<uint16_t> {
-  __device__ static float4 ld(const uint16_t* p) {
-    const uint2 u = *reinterpret_cast<const uint2*>(p);
-    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+// One 16-byte vector of channels: 4 fp32 or 8 bf16, widened to fp32.
+template <typename T> struct Vec;
+template <> struct Vec<float> {
+  static constexpr int N = 4;
+  __device__ static void unpack(uint4 u, float* v) {
+    v[0] = __uint_as_float(u.x); v[1] = __uint_as_float(u.y);
+    v[2] = __uint_as_float(u.z); v[3] = __uint_as_float(u.w);
   }
-  __device__ static void st(uint16_t* p, float4 v) {
-    uint2 u;
-    u.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
-    u.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
-    *reinterpret_cast<uint2*>(p) = u;
+  __device__ static void ld(const float* p, float* v) { unpack(*reinterpret_cast<const uint4*>(p), v); }
+  __device__ static void st(float* p, const float* v) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct Vec<uint16_t> {
+  static constexpr int N = 8;
+  __device__ static void ld(const uint16_t* p, float* v) { unpack(*reinterpret_cast<const uint4*>(p), v); }
+  __device__ static void unpack(uint4 u, float* v) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ static void st(uint16_t* p, const float* v) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
 
+// Thread layout shared by every BN kernel: a row of c channels is tpr =
+// c / VW threads (one vector group q each); a 256-thread block covers rpp =
+// 256 / tpr rows per pass (row phase rr).  No index division in the loops.
 struct ChunkGeom {
-  int64_t m;
-  int c;
   int rows_per_chunk;
   int nchunks;
 };
 
-static ChunkGeom chunk_geom(int64_t m, int c) {
+static int vec_width(int dtype) { return dtype == JR_BF16 ? 8 : 4; }
+
+static ChunkGeom chunk_geom(int64_t m, int c, int vw) {
+  const int tpr = c / vw;
+  const int rpp = std::max(1, 256 / tpr);
+  // one unrolled batch of rows per thread at least; at most kMaxChunks chunks
+  const int un = red_rows<0>();
+  int64_t rpc = std::max<int64_t>(ceil_div(m, kMaxChunks), (int64_t)rpp * un);
+  rpc = ceil_div(rpc, (int64_t)rpp * un) * rpp * un;
   ChunkGeom g;
-  g.m = m;
-  g.c = c;
-  int64_t rpc = ceil_div(m, kMaxChunks);
-  const int tpr = c / 4;                       // threads per row
-  const int rpp = tpr <= 256 ? 256 / tpr : 1;  // rows per pass
-  if (rpc < rpp) rpc = rpp;
-  const int64_t min_rows = ceil_div(16384, c);  // >= 64 KiB of fp32 input per block
-  if (rpc < min_rows) rpc = min_rows;
   g.rows_per_chunk = (int)rpc;
   g.nchunks = (int)ceil_div(m, rpc);
   return g;
 }
 
 // Per-chunk column sums.  MODE 0: (sum x, sum x^2).  MODE 1 (bwd):
-// (sum dy', sum dy'*xhat).  Thread layout: q = t % tpr is a float4 column
-// group, rr = t / tpr a row phase.  Partials: part[chunk][2][c] (fp64).
+// (sum dy', sum dy'*xhat).  Per-thread fp64 sums over a fixed row set,
+// fixed-order block combine: deterministic.  Loads stay packed (one uint4
+// per row and operand) until used, so red_rows<MODE>() rows are in flight
+// per thread: the loop is latency-bound, not bandwidth-bound, with fewer.
+// Partials: part[2][c][nchunks] (fp64, chunk-contiguous for the finalize).
 template <int MODE, typename T>
 __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, const T* __restrict__ dy,
                                                    int dy_off, int dy_stride, int64_t m, int c,
                                                    int rows_per_chunk, const float* __restrict__ mean,
                                                    const float* __restrict__ invstd,
                                                    const float* __restrict__ beta, double* part) {
-  __shared__ double red[256 * 8];
-  const int tpr = c >> 2;
+  constexpr int VW = Vec<T>::N;
+  constexpr int U = red_rows<MODE>();
+  __shared__ double red[256 * 2 * VW];
+  const int tpr = c / VW;
   const int rpp = 256 / tpr;
   const int t = threadIdx.x;
   const int q = t % tpr, rr = t / tpr;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
   const int64_t r1 = min(m, r0 + rows_per_chunk);
-  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+  double s0[VW], s1[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) s0[j] = s1[j] = 0.0;
   if (rr < rpp) {
-    float mu[4], is[4], be[4];
+    float mu[VW], is[VW], be[VW];
     if (MODE == 1) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        mu[j] = mean[q * 4 + j]; is[j] = invstd[q * 4 + j]; be[j] = beta[q * 4 + j];
+      for (int j = 0; j < VW; ++j) {
+        mu[j] = mean[q * VW + j]; is[j] = invstd[q * VW + j]; be[j] = beta[q * VW + j];
       }
     }
-    for (int64_t r = r0 + rr; r < r1; r += rpp) {
-      const float4 xv = V4<T>::ld(x + r * c + q * 4);
-      const float xa[4] = {xv.x, xv.y, xv.z, xv.w};
-      if (MODE == 0) {
+    const T* xp = x + q * VW;
+    const T* gp = MODE == 1 ? dy + dy_off + q * VW : nullptr;
+    for (int64_t r = r0 + rr; r < r1; r += (int64_t)rpp * U) {
+      uint4 xr[U], gr[U];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const double d = xa[j];
-          s0[j] += d;
-          s1[j] += d * d;
-        }
-      } else {
-        const float4 gv = V4<T>::ld(dy + r * dy_stride + dy_off + q * 4);
-        const float ga[4] = {gv.x, gv.y, gv.z, gv.w};
+      for (int u = 0; u < U; ++u) {
+        const int64_t ri = r + (int64_t)u * rpp;
+        const uint4 z = make_uint4(0, 0, 0, 0);   // zero bits = 0.0 in both dtypes: adds nothing
+        xr[u] = ri < r1 ? *reinterpret_cast<const uint4*>(xp + ri * c) : z;
+        if (MODE == 1) gr[u] = ri < r1 ? *reinterpret_cast<const uint4*>(gp + ri * dy_stride) : z;
+      }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float xh = bn_xhat(xa[j], mu[j], is[j]);
-          const float pre = __fadd_rn(xh, be[j]);
-          const float g = pre > 0.f ? ga[j] : 0.f;
-          s0[j] += (double)g;
-          s1[j] += (double)g * (double)xh;
+      for (int u = 0; u < U; ++u) {
+        float xv[VW];
+        Vec<T>::unpack(xr[u], xv);
+        if (MODE == 0) {
+#pragma unroll
+          for (int j = 0; j < VW; ++j) {
+            const double d = xv[j];
+            s0[j] += d;
+            s1[j] += d * d;
+          }
+        } else {
+          float gv[VW];
+          Vec<T>::unpack(gr[u], gv);
+#pragma unroll
+          for (int j = 0; j < VW; ++j) {
+            const float xh = bn_xhat(xv[j], mu[j], is[j]);
+            const float pre = __fadd_rn(xh, be[j]);
+            const float g = pre > 0.f ? gv[j] : 0.f;
+            s0[j] += (double)g;
+            s1[j] += (double)g * (double)xh;
+          }
         }
       }
     }
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    red[t * 8 + j] = s0[j];
-    red[t * 8 + 4 + j] = s1[j];
+  for (int j = 0; j < VW; ++j) {
+    red[t * 2 * VW + j] = s0[j];
+    red[t * 2 * VW + VW + j] = s1[j];
   }
   __syncthreads();
-  if (t < tpr) {
-    for (int k = 1; k < rpp; ++k) {
+  // fixed-shape tree over the row phases (log2(rpp) steps, deterministic)
+  int span = 1;
+  while (span < rpp) span <<= 1;
+  for (int s = span >> 1; s > 0; s >>= 1) {
+    if (rr < s && rr + s < rpp) {
+      double* a = red + t * 2 * VW;
+      const double* b = red + (t + s * tpr) * 2 * VW;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[t * 8 + j] += red[(k * tpr + t) * 8 + j];
+      for (int j = 0; j < 2 * VW; ++j) a[j] += b[j];
     }
-    double* pc = part + (int64_t)blockIdx.x * 2 * c;
+    __syncthreads();
+  }
+  if (t < tpr) {
+    const int64_t nch = gridDim.x;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      pc[q * 4 + j] = red[t * 8 + j];
-      pc[c + q * 4 + j] = red[t * 8 + 4 + j];
+    for (int j = 0; j < VW; ++j) {
+      part[(int64_t)(q * VW + j) * nch + blockIdx.x] = red[t * 2 * VW + j];
+      part[(int64_t)(c + q * VW + j) * nch + blockIdx.x] = red[t * 2 * VW + VW + j];
     }
   }
 }
 
 // Fixed-order combine of the chunk partials: one wave per channel; lane j
-// sums chunks j, j+64, ... (four loads in flight), then a fixed xor-butterfly
-// adds the 64 lane sums (deterministic, independent of timing).
+// sums chunks j, j+64, ... (coalesced, eight loads in flight), then a fixed
+// xor-butterfly adds the 64 lane sums (deterministic, independent of timing).
 // MODE 0: mean, invstd.   MODE 1: k1 = sum dy'/m, k2 = sum dy'xhat/m, dbeta.
 template <int MODE>
 __global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ part, int nchunks, int c,
@@ -150,17 +198,17 @@ __global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ 
   const int lane = threadIdx.x & 63;
   const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (k >= c) return;   // wave-uniform
-  const double* p0 = part + k;
-  const double* p1 = part + c + k;
-  const int64_t st = 2 * (int64_t)c;
-  double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-  int i = lane;
-  for (; i + 64 < nchunks; i += 128) {
-    const double x0 = p0[i * st], y0 = p1[i * st], x1 = p0[(i + 64) * st], y1 = p1[(i + 64) * st];
-    a0 += x0; b0 += y0; a1 += x1; b1 += y1;
+  const double* p0 = part + (int64_t)k * nchunks;
+  const double* p1 = part + (int64_t)(c + k) * nchunks;
+  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+  for (int i0 = 0; i0 < nchunks; i0 += 256) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * 64 + lane;
+      if (i < nchunks) { a[u] += p0[i]; b[u] += p1[i]; }
+    }
   }
-  if (i < nchunks) { a0 += p0[i * st]; b0 += p1[i * st]; }
-  double s0 = a0 + a1, s1 = b0 + b1;
+  double s0 = (a[0] + a[1]) + (a[2] + a[3]), s1 = (b[0] + b[1]) + (b[2] + b[3]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     s0 += __shfl_xor(s0, o, 64);
@@ -181,28 +229,40 @@ __global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ 
   }
 }
 
+// Elementwise passes: block b covers rows [b*rpp*U, (b+1)*rpp*U), thread
+// (q, rr) rows rr, rr+rpp, ...; per-channel constants loaded once.
 template <typename T>
 __global__ void __launch_bounds__(256) k_bn_relu_apply(const T* __restrict__ x, int64_t m, int c,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
                                                        const float* __restrict__ beta, T* y, int y_off,
                                                        int y_stride) {
-  const int c4 = c >> 2;
-  const int64_t total = m * c4;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / c4;
-    const int q = (int)(e - r * c4);
-    const float4 xv = V4<T>::ld(x + r * c + q * 4);
-    const float4 mu = *reinterpret_cast<const float4*>(mean + q * 4);
-    const float4 is = *reinterpret_cast<const float4*>(invstd + q * 4);
-    const float4 be = *reinterpret_cast<const float4*>(beta + q * 4);
-    float4 o;
-    o.x = fmaxf(bn_pre(xv.x, mu.x, is.x, be.x), 0.f);
-    o.y = fmaxf(bn_pre(xv.y, mu.y, is.y, be.y), 0.f);
-    o.z = fmaxf(bn_pre(xv.z, mu.z, is.z, be.z), 0.f);
-    o.w = fmaxf(bn_pre(xv.w, mu.w, is.w, be.w), 0.f);
-    V4<T>::st(y + r * y_stride + y_off + q * 4, o);
+  constexpr int VW = Vec<T>::N;
+  const int tpr = c / VW;
+  const int rpp = 256 / tpr;
+  const int t = threadIdx.x;
+  const int q = t % tpr, rr = t / tpr;
+  if (rr >= rpp) return;
+  float mu[VW], is[VW], be[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    mu[j] = mean[q * VW + j]; is[j] = invstd[q * VW + j]; be[j] = beta[q * VW + j];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpp * kAppUnroll + rr;
+  float xv[kAppUnroll][VW];
+#pragma unroll
+  for (int u = 0; u < kAppUnroll; ++u) {
+    const int64_t r = r0 + (int64_t)u * rpp;
+    if (r < m) Vec<T>::ld(x + r * c + q * VW, xv[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < kAppUnroll; ++u) {
+    const int64_t r = r0 + (int64_t)u * rpp;
+    if (r >= m) break;
+    float o[VW];
+#pragma unroll
+    for (int j = 0; j < VW; ++j) o[j] = fmaxf(bn_pre(xv[u][j], mu[j], is[j], be[j]), 0.f);
+    Vec<T>::st(y + r * y_stride + y_off + q * VW, o);
   }
 }
 
@@ -214,46 +274,69 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(const T* __restrict__
                                                            const float* __restrict__ beta,
                                                            const float* __restrict__ k1,
                                                            const float* __restrict__ k2, T* dx) {
-  const int c4 = c >> 2;
-  const int64_t total = m * c4;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / c4;
-    const int q = (int)(e - r * c4);
-    const float4 xv = V4<T>::ld(x + r * c + q * 4);
-    const float4 gv = V4<T>::ld(dy + r * dy_stride + dy_off + q * 4);
-    const float xa[4] = {xv.x, xv.y, xv.z, xv.w};
-    const float ga[4] = {gv.x, gv.y, gv.z, gv.w};
-    float o[4];
+  constexpr int VW = Vec<T>::N;
+  const int tpr = c / VW;
+  const int rpp = 256 / tpr;
+  const int t = threadIdx.x;
+  const int q = t % tpr, rr = t / tpr;
+  if (rr >= rpp) return;
+  float mu[VW], is[VW], be[VW], c1[VW], c2[VW];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = q * 4 + j;
-      const float is = invstd[k];
-      const float xh = bn_xhat(xa[j], mean[k], is);
-      const float pre = __fadd_rn(xh, beta[k]);
-      const float g = pre > 0.f ? ga[j] : 0.f;
-      o[j] = is * (g - k1[k] - xh * k2[k]);
+  for (int j = 0; j < VW; ++j) {
+    const int k = q * VW + j;
+    mu[j] = mean[k]; is[j] = invstd[k]; be[j] = beta[k]; c1[j] = k1[k]; c2[j] = k2[k];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpp * kAppUnroll + rr;
+  float xv[kAppUnroll][VW], gv[kAppUnroll][VW];
+#pragma unroll
+  for (int u = 0; u < kAppUnroll; ++u) {
+    const int64_t r = r0 + (int64_t)u * rpp;
+    if (r < m) {
+      Vec<T>::ld(x + r * c + q * VW, xv[u]);
+      Vec<T>::ld(dy + r * dy_stride + dy_off + q * VW, gv[u]);
     }
-    V4<T>::st(dx + r * c + q * 4, make_float4(o[0], o[1], o[2], o[3]));
+  }
+#pragma unroll
+  for (int u = 0; u < kAppUnroll; ++u) {
+    const int64_t r = r0 + (int64_t)u * rpp;
+    if (r >= m) break;
+    float o[VW];
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const float xh = bn_xhat(xv[u][j], mu[j], is[j]);
+      const float pre = __fadd_rn(xh, be[j]);
+      const float g = pre > 0.f ? gv[u][j] : 0.f;
+      o[j] = is[j] * (g - c1[j] - xh * c2[j]);
+    }
+    Vec<T>::st(dx + r * c + q * VW, o);
   }
 }
 
-static int grid_for(int64_t elems) {
-  const int64_t b = ceil_div(elems, 256);
-  return (int)std::min<int64_t>(std::max<int64_t>(b, 1), 256 * 16);
+static int apply_grid(int64_t m, int c, int vw) {
+  const int rpp = 256 / (c / vw);
+  return (int)ceil_div(m, (int64_t)rpp * kAppUnroll);
 }
 
 static int check_common(int dtype, int64_t m, int c) {
   if (dtype != JR_F32 && dtype != JR_BF16) return fail(JR_ERR_INVALID, "bn: bad dtype");
   if (m <= 0 || c <= 0) return fail(JR_ERR_INVALID, "bn: empty tensor");
-  if (c % 4 != 0) return fail(JR_ERR_INVALID, "bn: channel count must be a multiple of 4");
-  if (c / 4 > 256) return fail(JR_ERR_UNSUPPORTED, "bn: more than 1024 channels");
+  if (c % vec_width(dtype) != 0)
+    return fail(JR_ERR_INVALID, "bn: channel count must be a multiple of 4 (fp32) / 8 (bf16)");
+  if (c / vec_width(dtype) > 256) return fail(JR_ERR_UNSUPPORTED, "bn: more than 256 vectors per row");
   return JR_OK;
 }
 
+static int check_slice(int dtype, int off, int stride, int c) {
+  const int q = vec_width(dtype);
+  return off >= 0 && off + c <= stride && off % q == 0 && stride % q == 0;
+}
+
+// Partials for either dtype's geometry (the query carries no dtype).
 static size_t ws_need(int64_t m, int c) {
-  const ChunkGeom g = chunk_geom(m, c);
-  return (size_t)g.nchunks * 2 * c * sizeof(double) + 2 * (size_t)c * sizeof(float);
+  size_t n = 0;
+  for (int vw : {4, 8})
+    if (c % vw == 0) n = std::max(n, (size_t)chunk_geom(m, c, vw).nchunks);
+  return n * 2 * c * sizeof(double) + 2 * (size_t)c * sizeof(float);
 }
 
 }  // namespace jr
@@ -271,7 +354,7 @@ JR_API int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps
   if (rc) return rc;
   if (!x || !mean || !invstd) return fail(JR_ERR_INVALID, "bn_stats: null pointer");
   if (!ws || ws_bytes < ws_need(m, c)) return fail(JR_ERR_WORKSPACE, "bn_stats: workspace too small");
-  const ChunkGeom g = chunk_geom(m, c);
+  const ChunkGeom g = chunk_geom(m, c, vec_width(dtype));
   double* part = static_cast<double*>(ws);
   hipStream_t s = as_stream(stream);
   if (dtype == JR_F32)
@@ -294,10 +377,9 @@ JR_API int jr_bn_relu_apply(int dtype, const void* x, int64_t m, int32_t c, cons
   int rc = check_common(dtype, m, c);
   if (rc) return rc;
   if (!x || !mean || !invstd || !beta || !y) return fail(JR_ERR_INVALID, "bn_relu_apply: null pointer");
-  if (y_c_off < 0 || y_c_off + c > y_c_stride || (y_c_off % 4) || (y_c_stride % 4))
-    return fail(JR_ERR_INVALID, "bn_relu_apply: bad output slice");
+  if (!check_slice(dtype, y_c_off, y_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_apply: bad output slice");
   hipStream_t s = as_stream(stream);
-  const int grid = grid_for(m * (c / 4));
+  const int grid = apply_grid(m, c, vec_width(dtype));
   if (dtype == JR_F32)
     hipLaunchKernelGGL(k_bn_relu_apply<float>, dim3(grid), dim3(256), 0, s, (const float*)x, m, c, mean,
                        invstd, beta, (float*)y, y_c_off, y_c_stride);
@@ -314,10 +396,10 @@ JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t d
   if (rc) return rc;
   if (!dy || !x || !mean || !invstd || !beta || !dx || !dbeta)
     return fail(JR_ERR_INVALID, "bn_relu_bwd: null pointer");
-  if (dy_c_off < 0 || dy_c_off + c > dy_c_stride || (dy_c_off % 4) || (dy_c_stride % 4))
-    return fail(JR_ERR_INVALID, "bn_relu_bwd: bad dy slice");
+  if (!check_slice(dtype, dy_c_off, dy_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_bwd: bad dy slice");
   if (!ws || ws_bytes < ws_need(m, c)) return fail(JR_ERR_WORKSPACE, "bn_relu_bwd: workspace too small");
-  const ChunkGeom g = chunk_geom(m, c);
+  const int vw = vec_width(dtype);
+  const ChunkGeom g = chunk_geom(m, c, vw);
   double* part = static_cast<double*>(ws);
   float* k1 = reinterpret_cast<float*>(part + (size_t)g.nchunks * 2 * c);
   float* k2 = k1 + c;
@@ -336,7 +418,7 @@ JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t d
                      0.f, k1, k2, dbeta);
   rc = check_launch("bn_bwd finalize");
   if (rc) return rc;
-  const int grid = grid_for(m * (c / 4));
+  const int grid = apply_grid(m, c, vw);
   if (dtype == JR_F32)
     hipLaunchKernelGGL(k_bn_relu_bwd_apply<float>, dim3(grid), dim3(256), 0, s, (const float*)dy, dy_c_off,
                        dy_c_stride, (const float*)x, m, c, mean, invstd, beta, k1, k2, (float*)dx);
