@@ -94,6 +94,14 @@ size_t jr_conv2d_workspace_size(const jr_conv_desc* d, int op, int dtype);
 /* y[.., y_c_off + co] = sum x * w   (raw conv output, no bias) */
 int jr_conv2d_fwd(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y,
                   void* ws, size_t ws_bytes, void* stream);
+/* jr_conv2d_fwd fused with the training-mode BatchNormalization statistics
+ * of its output (Keras conv2d_bn: Conv2D -> BatchNormalization, App. C Q1):
+ * mean[co] = E[y], invstd[co] = 1/sqrt(biased var + eps) over n*ho*wo rows,
+ * of y as stored (bf16-rounded for JR_BF16).  Partial (mean, M2) per group
+ * of rows from the GEMM epilogue (or the split-K reduce), combined in fp64
+ * in a fixed order: deterministic.  Replaces jr_conv2d_fwd + jr_bn_stats. */
+int jr_conv2d_fwd_bn_stats(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y, float eps,
+                           float* mean, float* invstd, void* ws, size_t ws_bytes, void* stream);
 /* dx[.., x_c_off + ci] (+)= sum dy * w ; accumulate != 0 adds into dx */
 int jr_conv2d_bwd_data(const jr_conv_desc* d, int dtype, const void* dy, const void* w, void* dx,
                        int accumulate, void* ws, size_t ws_bytes, void* stream);
@@ -121,16 +129,19 @@ size_t jr_bn_workspace_size(int64_t m, int32_t c);
  * invstd = 1/sqrt(biased_var + eps). */
 int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps, float* mean, float* invstd,
                 void* ws, size_t ws_bytes, void* stream);
-/* y[.., y_c_off + k] = max((x - mean) * invstd + beta, 0) */
-int jr_bn_relu_apply(int dtype, const void* x, int64_t m, int32_t c, const float* mean,
-                     const float* invstd, const float* beta, void* y, int32_t y_c_off,
+/* y[.., y_c_off + k] = max((x[.., x_c_off + k] - mean) * invstd + beta, 0)
+ * (x: a channel slice of the raw conv output, e.g. one member of a fused
+ * sibling-conv group) */
+int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,
+                     const float* mean, const float* invstd, const float* beta, void* y, int32_t y_c_off,
                      int32_t y_c_stride, void* stream);
 /* Backward of apply+stats: dy is the gradient w.r.t. y (a channel slice),
- * dx [m][c] contiguous receives the gradient w.r.t. the raw conv output,
- * dbeta [c] receives sum of the ReLU-masked dy. */
+ * dx receives the gradient w.r.t. the raw conv output in the same channel
+ * slice geometry as x, dbeta [c] receives sum of the ReLU-masked dy. */
 int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t dy_c_stride, const void* x,
-                   int64_t m, int32_t c, const float* mean, const float* invstd, const float* beta,
-                   void* dx, float* dbeta, void* ws, size_t ws_bytes, void* stream);
+                   int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c, const float* mean,
+                   const float* invstd, const float* beta, void* dx, float* dbeta, void* ws, size_t ws_bytes,
+                   void* stream);
 
 /* ---- pooling (Keras MaxPooling2D((3,3),(2,2)) / AveragePooling2D((3,3),
  *      (1,1),'same') inside InceptionV3, train.py:129-130) ------------ */

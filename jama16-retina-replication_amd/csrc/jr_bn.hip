@@ -97,7 +97,7 @@ static ChunkGeom chunk_geom(int64_t m, int c, int vw) {
 // per thread: the loop is latency-bound, not bandwidth-bound, with fewer.
 // Partials: part[2][c][nchunks] (fp64, chunk-contiguous for the finalize).
 template <int MODE, typename T>
-__global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, const T* __restrict__ dy,
+__global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int xs, const T* __restrict__ dy,
                                                    int dy_off, int dy_stride, int64_t m, int c,
                                                    int rows_per_chunk, const float* __restrict__ mean,
                                                    const float* __restrict__ invstd,
@@ -130,7 +130,7 @@ __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, cons
       for (int u = 0; u < U; ++u) {
         const int64_t ri = r + (int64_t)u * rpp;
         const uint4 z = make_uint4(0, 0, 0, 0);   // zero bits = 0.0 in both dtypes: adds nothing
-        xr[u] = ri < r1 ? *reinterpret_cast<const uint4*>(xp + ri * c) : z;
+        xr[u] = ri < r1 ? *reinterpret_cast<const uint4*>(xp + ri * xs) : z;
         if (MODE == 1) gr[u] = ri < r1 ? *reinterpret_cast<const uint4*>(gp + ri * dy_stride) : z;
       }
 #pragma unroll
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ 
 // Elementwise passes: block b covers rows [b*rpp*U, (b+1)*rpp*U), thread
 // (q, rr) rows rr, rr+rpp, ...; per-channel constants loaded once.
 template <typename T>
-__global__ void __launch_bounds__(256) k_bn_relu_apply(const T* __restrict__ x, int64_t m, int c,
+__global__ void __launch_bounds__(256) k_bn_relu_apply(const T* __restrict__ x, int xs, int64_t m, int c,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
                                                        const float* __restrict__ beta, T* y, int y_off,
@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(256) k_bn_relu_apply(const T* __restrict__ x, 
 #pragma unroll
   for (int u = 0; u < kAppUnroll; ++u) {
     const int64_t r = r0 + (int64_t)u * rpp;
-    if (r < m) Vec<T>::ld(x + r * c + q * VW, xv[u]);
+    if (r < m) Vec<T>::ld(x + r * xs + q * VW, xv[u]);
   }
 #pragma unroll
   for (int u = 0; u < kAppUnroll; ++u) {
@@ -268,7 +268,7 @@ __global__ void __launch_bounds__(256) k_bn_relu_apply(const T* __restrict__ x, 
 
 template <typename T>
 __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(const T* __restrict__ dy, int dy_off, int dy_stride,
-                                                           const T* __restrict__ x, int64_t m, int c,
+                                                           const T* __restrict__ x, int xs, int64_t m, int c,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ beta,
@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(const T* __restrict__
   for (int u = 0; u < kAppUnroll; ++u) {
     const int64_t r = r0 + (int64_t)u * rpp;
     if (r < m) {
-      Vec<T>::ld(x + r * c + q * VW, xv[u]);
+      Vec<T>::ld(x + r * xs + q * VW, xv[u]);
       Vec<T>::ld(dy + r * dy_stride + dy_off + q * VW, gv[u]);
     }
   }
@@ -308,7 +308,7 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(const T* __restrict__
       const float g = pre > 0.f ? gv[u][j] : 0.f;
       o[j] = is[j] * (g - c1[j] - xh * c2[j]);
     }
-    Vec<T>::st(dx + r * c + q * VW, o);
+    Vec<T>::st(dx + r * xs + q * VW, o);
   }
 }
 
@@ -358,10 +358,10 @@ JR_API int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps
   double* part = static_cast<double*>(ws);
   hipStream_t s = as_stream(stream);
   if (dtype == JR_F32)
-    hipLaunchKernelGGL((k_bn_reduce<0, float>), dim3(g.nchunks), dim3(256), 0, s, (const float*)x,
+    hipLaunchKernelGGL((k_bn_reduce<0, float>), dim3(g.nchunks), dim3(256), 0, s, (const float*)x, c,
                        (const float*)nullptr, 0, 0, m, c, g.rows_per_chunk, nullptr, nullptr, nullptr, part);
   else
-    hipLaunchKernelGGL((k_bn_reduce<0, uint16_t>), dim3(g.nchunks), dim3(256), 0, s, (const uint16_t*)x,
+    hipLaunchKernelGGL((k_bn_reduce<0, uint16_t>), dim3(g.nchunks), dim3(256), 0, s, (const uint16_t*)x, c,
                        (const uint16_t*)nullptr, 0, 0, m, c, g.rows_per_chunk, nullptr, nullptr, nullptr,
                        part);
   rc = check_launch("bn_stats reduce");
@@ -371,31 +371,39 @@ JR_API int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps
   return check_launch("bn_stats finalize");
 }
 
-JR_API int jr_bn_relu_apply(int dtype, const void* x, int64_t m, int32_t c, const float* mean,
-                            const float* invstd, const float* beta, void* y, int32_t y_c_off,
+JR_API int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,
+                            const float* mean, const float* invstd, const float* beta, void* y, int32_t y_c_off,
                             int32_t y_c_stride, void* stream) {
   int rc = check_common(dtype, m, c);
   if (rc) return rc;
   if (!x || !mean || !invstd || !beta || !y) return fail(JR_ERR_INVALID, "bn_relu_apply: null pointer");
+  if (!check_slice(dtype, x_c_off, x_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_apply: bad input slice");
+  const size_t esz = dtype == JR_BF16 ? 2 : 4;
+  x = static_cast<const char*>(x) + (size_t)x_c_off * esz;
   if (!check_slice(dtype, y_c_off, y_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_apply: bad output slice");
   hipStream_t s = as_stream(stream);
   const int grid = apply_grid(m, c, vec_width(dtype));
   if (dtype == JR_F32)
-    hipLaunchKernelGGL(k_bn_relu_apply<float>, dim3(grid), dim3(256), 0, s, (const float*)x, m, c, mean,
+    hipLaunchKernelGGL(k_bn_relu_apply<float>, dim3(grid), dim3(256), 0, s, (const float*)x, x_c_stride, m, c, mean,
                        invstd, beta, (float*)y, y_c_off, y_c_stride);
   else
-    hipLaunchKernelGGL(k_bn_relu_apply<uint16_t>, dim3(grid), dim3(256), 0, s, (const uint16_t*)x, m, c,
+    hipLaunchKernelGGL(k_bn_relu_apply<uint16_t>, dim3(grid), dim3(256), 0, s, (const uint16_t*)x, x_c_stride, m, c,
                        mean, invstd, beta, (uint16_t*)y, y_c_off, y_c_stride);
   return check_launch("bn_relu_apply");
 }
 
 JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t dy_c_stride, const void* x,
-                          int64_t m, int32_t c, const float* mean, const float* invstd, const float* beta,
-                          void* dx, float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+                          int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c, const float* mean,
+                          const float* invstd, const float* beta, void* dx, float* dbeta, void* ws, size_t ws_bytes,
+                          void* stream) {
   int rc = check_common(dtype, m, c);
   if (rc) return rc;
   if (!dy || !x || !mean || !invstd || !beta || !dx || !dbeta)
     return fail(JR_ERR_INVALID, "bn_relu_bwd: null pointer");
+  if (!check_slice(dtype, x_c_off, x_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_bwd: bad x / dx slice");
+  const size_t esz = dtype == JR_BF16 ? 2 : 4;
+  x = static_cast<const char*>(x) + (size_t)x_c_off * esz;
+  dx = static_cast<char*>(dx) + (size_t)x_c_off * esz;
   if (!check_slice(dtype, dy_c_off, dy_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_bwd: bad dy slice");
   if (!ws || ws_bytes < ws_need(m, c)) return fail(JR_ERR_WORKSPACE, "bn_relu_bwd: workspace too small");
   const int vw = vec_width(dtype);
@@ -405,12 +413,12 @@ JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t d
   float* k2 = k1 + c;
   hipStream_t s = as_stream(stream);
   if (dtype == JR_F32)
-    hipLaunchKernelGGL((k_bn_reduce<1, float>), dim3(g.nchunks), dim3(256), 0, s, (const float*)x,
+    hipLaunchKernelGGL((k_bn_reduce<1, float>), dim3(g.nchunks), dim3(256), 0, s, (const float*)x, x_c_stride,
                        (const float*)dy, dy_c_off, dy_c_stride, m, c, g.rows_per_chunk, mean, invstd, beta,
                        part);
   else
     hipLaunchKernelGGL((k_bn_reduce<1, uint16_t>), dim3(g.nchunks), dim3(256), 0, s, (const uint16_t*)x,
-                       (const uint16_t*)dy, dy_c_off, dy_c_stride, m, c, g.rows_per_chunk, mean, invstd,
+                       x_c_stride, (const uint16_t*)dy, dy_c_off, dy_c_stride, m, c, g.rows_per_chunk, mean, invstd,
                        beta, part);
   rc = check_launch("bn_bwd reduce");
   if (rc) return rc;
@@ -421,10 +429,10 @@ JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t d
   const int grid = apply_grid(m, c, vw);
   if (dtype == JR_F32)
     hipLaunchKernelGGL(k_bn_relu_bwd_apply<float>, dim3(grid), dim3(256), 0, s, (const float*)dy, dy_c_off,
-                       dy_c_stride, (const float*)x, m, c, mean, invstd, beta, k1, k2, (float*)dx);
+                       dy_c_stride, (const float*)x, x_c_stride, m, c, mean, invstd, beta, k1, k2, (float*)dx);
   else
     hipLaunchKernelGGL(k_bn_relu_bwd_apply<uint16_t>, dim3(grid), dim3(256), 0, s, (const uint16_t*)dy,
-                       dy_c_off, dy_c_stride, (const uint16_t*)x, m, c, mean, invstd, beta, k1, k2,
+                       dy_c_off, dy_c_stride, (const uint16_t*)x, x_c_stride, m, c, mean, invstd, beta, k1, k2,
                        (uint16_t*)dx);
   return check_launch("bn_bwd apply");
 }

@@ -69,7 +69,8 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int A_INSTR = ASZ / 256, B_INSTR = BSZ / 256;
   constexpr int A_PW = (A_INSTR + 3) / 4, B_PW = (B_INSTR + 3) / 4;  // per wave
   static_assert(ASZ % 256 == 0 && BSZ % 256 == 0, "tile must be whole DMA instructions");
-  __shared__ __attribute__((aligned(1024))) float smem[NBUF * (ASZ + BSZ)];
+  constexpr int SMEM = NBUF * (ASZ + BSZ) > 4 * stage_floats<WN>() ? NBUF * (ASZ + BSZ) : 4 * stage_floats<WN>();
+  __shared__ __attribute__((aligned(1024))) float smem[SMEM];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -425,27 +426,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   }
 
   // ---------------------------------------------------------------- epilogue
-  const bool split = gridDim.z > 1;
-  float* C = split ? g.C + (long long)blockIdx.z * g.slab_elems : g.C;
-  const int rbase = 4 * lh;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
-      if (m >= g.M) continue;
-      const long long base = split ? (long long)m * g.N : out_row<OP>(g, m);
-      if (base < 0) continue;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn0 + j * 32 + l31;
-        if (n >= g.N) continue;
-        float* p = C + base + n;
-        if (!split && g.accumulate) *p += acc[i][j][r];
-        else *p = acc[i][j][r];
-      }
-    }
-  }
+  conv_epilogue<OP, WM, TM, TN, false>(g, acc, smem + wave * stage_floats<WN>(), m0 + wm0, n0 + wn0, lane);
 }
 
 // ---------------------------------------------------------------- host side
@@ -555,6 +536,37 @@ static size_t plan_ws(const Plan& p) {
   return p.splits > 1 ? (size_t)p.splits * (size_t)p.M * (size_t)p.N * sizeof(float) : 0;
 }
 
+// Fused BN statistics (FWD): partials of R rows each, P per column.  Without
+// split-K the GEMM epilogue writes one per wave row-group (R = WM); with it,
+// k_splitk_reduce_stats one per block of R rows (~512 blocks).
+struct StatsReq {
+  float eps;
+  float* mean;
+  float* invstd;
+};
+
+static void stats_geom(int dtype, const Plan& p, int* P, int* R) {
+  const TileCfg& t = cfg_table(dtype)[p.tile];
+  if (p.splits <= 1) {
+    *R = t.bm / t.wgm;
+    *P = p.mt * t.wgm;
+    return;
+  }
+  const int rpp = 256 / (std::min(p.N, 1024) / 4);
+  int r = std::max<int>(rpp, (int)ceil_div(p.M, 512));
+  r = (int)ceil_div(r, rpp) * rpp;
+  *R = r;
+  *P = (int)ceil_div(p.M, r);
+}
+
+static size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+
+static size_t stats_ws(int dtype, const Plan& p) {
+  int P, R;
+  stats_geom(dtype, p, &P, &R);
+  return 2 * (size_t)p.N * P * sizeof(float);
+}
+
 // Fast-path kernels (UT): FWD/DGRAD when the reduction channel radix is a
 // multiple of BK (every layer but conv1 FWD at BK = 16); WGRAD when wo >= BK.
 template <int OP, int C, int DBG>
@@ -632,8 +644,17 @@ static void fill_common(ConvArgs& a, const jr_conv_desc* d, int dtype) {
 
 // One GEMM (plus its split-K reduce) on the stream.
 template <int OP>
-static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, size_t ws_bytes, hipStream_t s) {
+static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, size_t ws_bytes, hipStream_t s,
+                    const StatsReq* st = nullptr) {
   if (p.M <= 0 || p.N <= 0) return JR_OK;
+  int sP = 0, sR = 0;
+  if (st) {
+    stats_geom(dtype, p, &sP, &sR);
+    const size_t off = align256(plan_ws(p));
+    if (!ws || ws_bytes < off + stats_ws(dtype, p)) return fail(JR_ERR_WORKSPACE, "conv: workspace too small for BN statistics");
+    a.stats = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
+    a.stats_p = sP;
+  }
   a.M = p.M; a.N = p.N; a.K = p.K;
   a.ktiles = p.ktiles;
   a.kt_per_split = p.kt_per_split;
@@ -654,7 +675,23 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     launch_op<OP>(p.tile, a, grid, s);
   }
   int rc = check_launch("conv gemm");
-  if (rc || p.splits <= 1) return rc;
+  if (rc) return rc;
+  if (st) {
+    if (p.splits > 1) {
+      if (dtype == JR_BF16)
+        hipLaunchKernelGGL((k_splitk_reduce_stats<uint16_t>), dim3(sP, (int)ceil_div(p.N, 1024)), dim3(256), 0, s, (const float*)ws, p.splits, a,
+                           static_cast<uint16_t*>(out), sR);
+      else
+        hipLaunchKernelGGL((k_splitk_reduce_stats<float>), dim3(sP, (int)ceil_div(p.N, 1024)), dim3(256), 0, s, (const float*)ws, p.splits, a,
+                           static_cast<float*>(out), sR);
+      rc = check_launch("conv split-k reduce + stats");
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_stats_finalize, dim3(p.N), dim3(256), 0, s, (const float*)a.stats, sP, sR, p.M, p.N,
+                       st->eps, st->mean, st->invstd);
+    return check_launch("conv stats finalize");
+  }
+  if (p.splits <= 1) return rc;
   const long long total = (long long)p.M * p.N / 4;   // float4 columns
   int G = 1;                                            // z-lanes per column
   while (G < 64 && G * 4 <= p.splits && total * G < 128 * 1024) G *= 2;
@@ -688,19 +725,28 @@ static size_t ws_bytes_for(const jr_conv_desc* d, int op, int dtype) {
   Phase ph[64];
   int nph = 1;
   if (op == OP_DGRAD) dgrad_phases(d, ph, &nph);
-  size_t w = 0;
+  size_t w = 0, sw = 0;
   for (int i = 0; i < nph; ++i) {
     if (op == OP_DGRAD && (ph[i].na == 0 || ph[i].nb == 0 || ph[i].hc == 0 || ph[i].wc == 0)) continue;
-    for (int c = 0; c < cfg_count(dtype); ++c)
-      w = std::max(w, plan_ws(plan_for(d, op, dtype, op == OP_DGRAD ? &ph[i] : nullptr, c)));
+    for (int c = 0; c < cfg_count(dtype); ++c) {
+      const Plan p = plan_for(d, op, dtype, op == OP_DGRAD ? &ph[i] : nullptr, c);
+      w = std::max(w, plan_ws(p));
+      if (op == OP_FWD) {   // fused BN statistics partials, split or not
+        Plan p1 = p;
+        p1.splits = 1;
+        sw = std::max(sw, std::max(stats_ws(dtype, p), stats_ws(dtype, p1)));
+      }
+    }
   }
-  return 2 * w;   // room for the autotuner's doubled split-K factors
+  // 2x: room for the autotuner's doubled split-K factors; FWD: the statistics
+  // partials live behind the slabs
+  return op == OP_FWD ? align256(2 * w) + sw : 2 * w;
 }
 
 // Runs the op; force_cfg >= 0 overrides the plan (autotuning).
 static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, const void* B, void* C,
                     int accumulate, void* ws, size_t ws_bytes, void* stream, int force_cfg = -1,
-                    int only_phase = -1) {
+                    int only_phase = -1, const StatsReq* st = nullptr) {
   int rc = validate(d, op, dtype);
   if (rc) return rc;
   if (!A || !B || !C) return fail(JR_ERR_INVALID, "conv: null tensor pointer");
@@ -715,7 +761,7 @@ static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, con
   void* out = C;
   if (op == OP_FWD) {
     a.c_off = d->y_c_off; a.c_stride = d->y_c_stride;
-    return run_gemm<OP_FWD>(dtype, a, plan_for(d, op, dtype, nullptr, force_cfg), out, ws, ws_bytes, s);
+    return run_gemm<OP_FWD>(dtype, a, plan_for(d, op, dtype, nullptr, force_cfg), out, ws, ws_bytes, s, st);
   }
   if (op == OP_WGRAD) {
     a.c_off = 0; a.c_stride = d->c_out;
@@ -767,7 +813,9 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
     int best_c = heuristic_cfg(dtype, M, N, K);
     float best_t = 1e30f;
     auto time_cfg = [&](int c) -> float {
-      if (plan_ws(plan_with(dtype, c, M, N, K)) > ws_bytes) return 1e30f;
+      const Plan pc = plan_with(dtype, c, M, N, K);
+      // FWD runs with the fused BN statistics: their partials must fit too
+      if ((op == OP_FWD ? align256(plan_ws(pc)) + stats_ws(dtype, pc) : plan_ws(pc)) > ws_bytes) return 1e30f;
       rc = run_conv(d, op, dtype, A, B, C, 0, ws, ws_bytes, stream, c, op == OP_DGRAD ? i : -1);  // warm-up
       if (rc) return 1e30f;
       (void)hipEventRecord(e0, s);
@@ -809,9 +857,61 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
   return rc;
 }
 
+__global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict__ part, int P, int R, int M, int N,
+                                                        float eps, float* mean, float* invstd) {
+  __shared__ double red[256];
+  const int n = blockIdx.x, t = threadIdx.x;
+  const float* pm = part + (long long)n * P;
+  const float* pq = part + (long long)(N + n) * P;
+  auto cnt = [&](int i) { return (double)min(max(M - i * R, 0), R); };
+  auto tree = [&](double v) {
+    red[t] = v;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+      if (t < h) red[t] += red[t + h];
+      __syncthreads();
+    }
+    const double r = red[0];
+    __syncthreads();
+    return r;
+  };
+  double a[4] = {0, 0, 0, 0};
+  for (int i0 = 0; i0 < P; i0 += 1024) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * 256 + t;
+      if (i < P) a[u] += cnt(i) * (double)pm[i];
+    }
+  }
+  const double mu = tree((a[0] + a[1]) + (a[2] + a[3])) / (double)M;
+  double b[4] = {0, 0, 0, 0};
+  for (int i0 = 0; i0 < P; i0 += 1024) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * 256 + t;
+      if (i < P) {
+        const double d = (double)pm[i] - mu;
+        b[u] += (double)pq[i] + cnt(i) * d * d;
+      }
+    }
+  }
+  const double m2 = tree((b[0] + b[1]) + (b[2] + b[3]));
+  if (t == 0) {
+    mean[n] = (float)mu;
+    invstd[n] = (float)(1.0 / sqrt(m2 / (double)M + (double)eps));
+  }
+}
+
 }  // namespace jr
 
 using namespace jr;
+
+JR_API int jr_conv2d_fwd_bn_stats(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y, float eps,
+                                  float* mean, float* invstd, void* ws, size_t ws_bytes, void* stream) {
+  if (!mean || !invstd) return fail(JR_ERR_INVALID, "conv fwd+stats: null statistics pointer");
+  const StatsReq st{eps, mean, invstd};
+  return run_conv(d, OP_FWD, dtype, x, w, y, 0, ws, ws_bytes, stream, -1, -1, &st);
+}
 
 JR_API size_t jr_conv2d_workspace_size(const jr_conv_desc* d, int op, int dtype) {
   if (!d || validate(d, op, dtype) != JR_OK) return 0;

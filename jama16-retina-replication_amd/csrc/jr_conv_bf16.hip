@@ -46,7 +46,8 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   constexpr int A_PW = (A_INSTR + 3) / 4, B_PW = (B_INSTR + 3) / 4;  // per wave
   static_assert(ASZ % 512 == 0 && BSZ % 512 == 0, "tile must be whole DMA instructions");
   static_assert(BK % 16 == 0 && QPR <= 8, "BK must be 16..64");
-  __shared__ __attribute__((aligned(1024))) uint16_t smem[NBUF * (ASZ + BSZ)];
+  constexpr int SMEM = NBUF * (ASZ + BSZ) > 8 * stage_floats<WN>() ? NBUF * (ASZ + BSZ) : 8 * stage_floats<WN>();
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[SMEM];
 
   const uint16_t* __restrict__ gA = reinterpret_cast<const uint16_t*>(g.A);
   const uint16_t* __restrict__ gB = reinterpret_cast<const uint16_t*>(g.B);
@@ -362,33 +363,8 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   }
 
   // ---------------------------------------------------------------- epilogue
-  const bool split = gridDim.z > 1;
-  const int rbase = 4 * lh;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm0 + i * 32 + (r & 3) + 8 * (r >> 2) + rbase;
-      if (m >= g.M) continue;
-      const long long base = split ? (long long)m * g.N : out_row<OP>(g, m);
-      if (base < 0) continue;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn0 + j * 32 + l31;
-        if (n >= g.N) continue;
-        if (split) {
-          g.C[(long long)blockIdx.z * g.slab_elems + base + n] = acc[i][j][r];
-        } else if constexpr (OP == OP_WGRAD) {
-          g.C[base + n] = acc[i][j][r];
-        } else {
-          uint16_t* p = reinterpret_cast<uint16_t*>(g.C) + base + n;
-          float v = acc[i][j][r];
-          if (g.accumulate) v += bf2f(*p);
-          *p = f2bf(v);
-        }
-      }
-    }
-  }
+  conv_epilogue<OP, WM, TM, TN, true>(g, acc, reinterpret_cast<float*>(smem) + wave * stage_floats<WN>(), m0 + wm0,
+                                      n0 + wn0, lane);
 }
 
 template <int OP, int C>

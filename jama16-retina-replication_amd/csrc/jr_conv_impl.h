@@ -25,6 +25,10 @@ struct ConvArgs {
   int accumulate;
   int ktiles, kt_per_split, ntn;
   long long slab_elems;       // M*N (split-K slabs)
+  // FWD only: fused BatchNorm statistics partials (nullptr = none), laid out
+  // stats[2][N][stats_p]: per-column (mean, M2) of each group of WM rows
+  float* stats;
+  int stats_p;
   // DGRAD phase (py,px): taps r = r0 + sh*a (a < na), c = c0 + sw*b (b < nb);
   // m = (b, u, v) over hc x wc; ih = sh*u + py; oh = u + ey - a.
   int py, px, r0, c0, na, nb, ey, ex, hc, wc;
@@ -94,6 +98,112 @@ __device__ __forceinline__ void adv_mixed_t(int& x, int& y, int& z, int lx, int 
 __device__ __forceinline__ void dma16(const void* src, void* lds_chunk) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_chunk, 16, 0, 0);
+}
+
+// ---------------------------------------------------------------- epilogue
+// A wave's WM x WN accumulator tile leaves 32 rows at a time through the
+// wave's own LDS region [32][WN + 8] fp32 (the two 32-lane halves of a store
+// are 4 rows = 32 banks apart, so they do not collide) and is written as
+// 8-element row vectors per lane: 32 B fp32 or 16 B bf16, whole row segments
+// per wave-instruction, and one vector read-modify-write per lane when
+// accumulating into dx (per-element 2-byte bf16 stores and RMW were the
+// epilogue's cost before).  FWD with g.stats (no split-K): per-column BN
+// statistics of the wave's rows, as stored (bf16-rounded for bf16 outputs):
+// mean and M2 = sum (v - mean)^2 (two passes over the registers), combined
+// in fp64 by k_stats_finalize.
+template <int WN> constexpr int stage_floats() { return 32 * (WN + 8); }
+
+template <int OP, int WM, int TM, int TN, bool BF16K>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& g, f32x16 (&acc)[TM][TN], float* stage, int mw0,
+                                              int nw0, int lane) {
+  constexpr int WN = TN * 32, S = WN + 8, LPR = WN / 8, NIT = 32 * LPR / 64;
+  static_assert((32 * LPR) % 64 == 0, "stage read-back must be whole wave-instructions");
+  const bool split = gridDim.z > 1;
+  const bool bout = BF16K && OP != OP_WGRAD && !split;
+  const int l31 = lane & 31, lh = lane >> 5;
+  auto row_of = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * lh; };
+  if constexpr (OP == OP_FWD) {
+    if (g.stats != nullptr && !split) {
+      const int P = g.stats_p;
+      const int pidx = mw0 / WM;
+      const int nv = min(max(g.M - mw0, 0), WM);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float v = acc[i][j][r];
+            if (bout) { v = bf2f(f2bf(v)); acc[i][j][r] = v; }
+            s += (mw0 + i * 32 + row_of(r) < g.M) ? v : 0.f;
+          }
+        s += __shfl_xor(s, 32, 64);
+        const float mu = nv > 0 ? s / (float)nv : 0.f;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float d = acc[i][j][r] - mu;
+            q += (mw0 + i * 32 + row_of(r) < g.M) ? d * d : 0.f;
+          }
+        q += __shfl_xor(q, 32, 64);
+        const int n = nw0 + j * 32 + l31;
+        if (lh == 0 && n < g.N) {
+          g.stats[(long long)n * P + pidx] = mu;
+          g.stats[(long long)(g.N + n) * P + pidx] = q;
+        }
+      }
+    }
+  }
+  float* C = split ? g.C + (long long)blockIdx.z * g.slab_elems : g.C;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) stage[row_of(r) * S + j * 32 + l31] = acc[i][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = it * 64 + lane;
+      const int row = e / LPR, c8 = (e - row * LPR) * 8;
+      const float4 v0 = *reinterpret_cast<const float4*>(stage + row * S + c8);
+      const float4 v1 = *reinterpret_cast<const float4*>(stage + row * S + c8 + 4);
+      const int m = mw0 + i * 32 + row, n = nw0 + c8;
+      if (m >= g.M || n >= g.N) continue;
+      const long long base = split ? (long long)m * g.N : out_row<OP>(g, m);
+      if (base < 0) continue;
+      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      if (bout) {
+        uint4* p = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + base + n);
+        if (g.accumulate) {
+          const uint4 o = *p;
+          const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[2 * k] += __uint_as_float(w[k] << 16);
+            v[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+          }
+        }
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16);
+        *p = make_uint4(w[0], w[1], w[2], w[3]);
+      } else {
+        float4* p = reinterpret_cast<float4*>(C + base + n);
+        if (!split && g.accumulate) {
+          const float4 o0 = p[0], o1 = p[1];
+          v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w;
+          v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
+        }
+        p[0] = make_float4(v[0], v[1], v[2], v[3]);
+        p[1] = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
 }
 
 // out[out_row(m) + n] (+)= sum_z slab[z][m][n], float4 along n (N % 16 == 0
@@ -166,6 +276,113 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
     }
   }
 }
+
+// FWD split-K reduce with fused BN statistics.  Block (b, y) owns rows
+// [b*R, (b+1)*R) (so its statistics partial covers exactly those rows) of
+// columns [1024 y, 1024 y + 1024), thread (q, rr) one float4 column group q
+// and rows rr, rr+rpp, ...; the
+// output is written as in k_splitk_reduce (bf16 rounded once).  Per thread
+// shifted sums about its first value, then (count, mean, M2) combined over
+// the row phases by a fixed-shape Chan tree: deterministic.
+template <typename TO>
+__global__ void __launch_bounds__(256) k_splitk_reduce_stats(const float* __restrict__ slab, int splits, ConvArgs g,
+                                                             TO* out, int R) {
+  __shared__ float s_n[256];
+  __shared__ float4 s_mu[256], s_m2[256];
+  const int cb = blockIdx.y * 1024;
+  const int tpr = min(1024, g.N - cb) >> 2;
+  const int rpp = 256 / tpr;
+  const int t = threadIdx.x;
+  const int q = t % tpr, rr = t / tpr;
+  const int c0 = cb + q * 4;
+  const int r0 = blockIdx.x * R, r1 = min(g.M, r0 + R);
+  float kk[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f}, a2[4] = {0.f, 0.f, 0.f, 0.f};
+  int cnt = 0;
+  if (rr < rpp) {
+    for (int m = r0 + rr; m < r1; m += rpp) {
+      const float4* src = reinterpret_cast<const float4*>(slab + (long long)m * g.N + c0);
+      const long long zs = g.slab_elems >> 2;
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      int z = 0;
+      for (; z + 3 < splits; z += 4) {
+        const float4 a = src[z * zs], b = src[(z + 1) * zs], c = src[(z + 2) * zs], d = src[(z + 3) * zs];
+        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+        s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+        s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
+        s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
+      }
+      for (; z < splits; ++z) {
+        const float4 a = src[z * zs];
+        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+      }
+      float v[4] = {s.x, s.y, s.z, s.w};
+      TO* p = out + out_row<OP_FWD>(g, m) + c0;
+      if constexpr (sizeof(TO) == 4) {
+        *reinterpret_cast<float4*>(p) = s;
+      } else {
+        const uint16_t b0 = f2bf(v[0]), b1 = f2bf(v[1]), b2 = f2bf(v[2]), b3 = f2bf(v[3]);
+        *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)b0 | ((uint32_t)b1 << 16), (uint32_t)b2 | ((uint32_t)b3 << 16));
+        v[0] = bf2f(b0); v[1] = bf2f(b1); v[2] = bf2f(b2); v[3] = bf2f(b3);
+      }
+      if (cnt == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kk[j] = v[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[j] - kk[j];
+        a1[j] += d;
+        a2[j] = fmaf(d, d, a2[j]);
+      }
+      ++cnt;
+    }
+  }
+  float mu[4], m2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    mu[j] = cnt ? kk[j] + a1[j] / (float)cnt : 0.f;
+    m2[j] = cnt ? fmaxf(a2[j] - a1[j] * a1[j] / (float)cnt, 0.f) : 0.f;
+  }
+  s_n[t] = (float)cnt;
+  s_mu[t] = make_float4(mu[0], mu[1], mu[2], mu[3]);
+  s_m2[t] = make_float4(m2[0], m2[1], m2[2], m2[3]);
+  __syncthreads();
+  int span = 1;
+  while (span < rpp) span <<= 1;
+  for (int h = span >> 1; h > 0; h >>= 1) {
+    if (rr < h && rr + h < rpp) {
+      const int o = t + h * tpr;
+      const float na = s_n[t], nb = s_n[o], nn = na + nb;
+      if (nb > 0.f) {
+        const float4 ma = s_mu[t], mb = s_mu[o], qa = s_m2[t], qb = s_m2[o];
+        const float fa = na / nn, fb = nb / nn, w = na * nb / nn;
+        const float dx = mb.x - ma.x, dy = mb.y - ma.y, dz = mb.z - ma.z, dw = mb.w - ma.w;
+        s_mu[t] = make_float4(ma.x * fa + mb.x * fb, ma.y * fa + mb.y * fb, ma.z * fa + mb.z * fb, ma.w * fa + mb.w * fb);
+        s_m2[t] = make_float4(qa.x + qb.x + dx * dx * w, qa.y + qb.y + dy * dy * w, qa.z + qb.z + dz * dz * w,
+                              qa.w + qb.w + dw * dw * w);
+        s_n[t] = nn;
+      }
+    }
+    __syncthreads();
+  }
+  if (rr == 0) {
+    const int P = gridDim.x;
+    const float4 a = s_mu[t], b = s_m2[t];
+    const float am[4] = {a.x, a.y, a.z, a.w}, bm[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      g.stats[(long long)(c0 + j) * P + blockIdx.x] = am[j];
+      g.stats[(long long)(g.N + c0 + j) * P + blockIdx.x] = bm[j];
+    }
+  }
+}
+
+// (mean, invstd) per channel from stats[2][N][P] partials of R rows each
+// (the last ones hold fewer, down to 0): mean = sum n_i mean_i / M, then
+// M2 = sum M2_i + n_i (mean_i - mean)^2, both in fp64 with a fixed-shape
+// tree; invstd = 1/sqrt(M2/M + eps) (biased variance, TF FusedBatchNorm).
+__global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict__ part, int P, int R, int M, int N,
+                                                        float eps, float* mean, float* invstd);
 
 struct TileCfg {
   int bm, bn, wgm, bk, nbuf;

@@ -55,6 +55,8 @@ _SIGS = {
     "jr_conv2d_workspace_size": (c_size_t, [POINTER(ConvDesc), c_int, c_int]),
     "jr_conv2d_fwd": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_size_t, c_void_p]),
+    "jr_conv2d_fwd_bn_stats": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_float,
+                                       c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_bwd_data": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_int,
                                    c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_bwd_filter": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p,
@@ -72,9 +74,9 @@ _SIGS = {
     "jr_bn_workspace_size": (c_size_t, [c_int64, c_int32]),
     "jr_bn_stats": (c_int, [c_int, c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
                             c_void_p, c_size_t, c_void_p]),
-    "jr_bn_relu_apply": (c_int, [c_int, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p,
-                                 c_void_p, c_int32, c_int32, c_void_p]),
-    "jr_bn_relu_bwd": (c_int, [c_int, c_void_p, c_int32, c_int32, c_void_p, c_int64, c_int32,
+    "jr_bn_relu_apply": (c_int, [c_int, c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "jr_bn_relu_bwd": (c_int, [c_int, c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_size_t, c_void_p]),
     "jr_maxpool3x3s2_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p,

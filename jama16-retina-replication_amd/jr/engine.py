@@ -6,11 +6,14 @@ blocks, head + loss, backward, and 190 ApplyMomentum updates.  This module is
 that step, MI355X-native:
 
 * All device memory is planned once per (batch, resolution): one NHWC buffer
-  per block output (concat-free slices), a raw pre-BN buffer per conv (kept
-  for the BN backward), one gradient buffer per activation buffer, a flat fp32
-  parameter / gradient / momentum buffer (so one optimizer launch and one
-  all-reduce bucket walk cover all 190 tensors).  PyTorch tensors are used
-  only as owners of that memory; every op is a libjr C-ABI call.
+  per block output (concat-free slices), a raw pre-BN buffer per conv launch
+  (kept for the BN backward), one gradient buffer per activation buffer, a
+  flat fp32 parameter / gradient / momentum buffer (so one optimizer launch
+  and one all-reduce bucket walk cover all 190 tensors).  PyTorch tensors are
+  used only as owners of that memory; every op is a libjr C-ABI call.
+* Conv launches follow jr.plan: sibling 1x1 layers reading one buffer run as
+  one fused GEMM (their kernels stored side by side), each member keeping its
+  own BN, beta and output slice.
 * Calls are pre-bound (ctypes function + argument tuple) into call lists, so a
   step is a flat loop of C calls on one HIP stream, and the whole step can be
   captured into a HIP graph (jr_graph_*) and replayed.
@@ -27,8 +30,9 @@ import numpy as np
 import torch
 
 from . import _ffi
-from .inception import BN_EPS, ConvNode, Graph, PoolNode, build_inception_v3
-from .init import init_params, param_layout
+from .inception import BN_EPS, Graph, PoolNode, build_inception_v3
+from .init import init_params
+from .plan import ConvUnit, build_plan
 
 DTYPES = {"f32": _ffi.JR_F32, "bf16": _ffi.JR_BF16}
 
@@ -40,7 +44,7 @@ class Engine:
                  device: int | torch.device = 0, dtype: str = "f32", train: bool = True,
                  optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
                  head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None,
-                 autotune: bool = True):
+                 autotune: bool = True, fuse_siblings: bool = True):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if not torch.cuda.is_available():
@@ -60,8 +64,9 @@ class Engine:
         self.units = self.g.units
         self.stream = torch.cuda.Stream(device=self.device)
         self._s = ctypes.c_void_p(self.stream.cuda_stream)
-        self.layout, self.nparam = param_layout(self.g.params)
-        self.poffs = {name: (off, size) for name, _, off, size in self.layout}
+        self.plan = build_plan(self.g, fuse_siblings)
+        self.cunits: List[ConvUnit] = self.plan.units
+        self.layout, self.nparam = self.plan.layout, self.plan.nparam
         self._alloc()
         self.load_params(init_params(self.g, seed))
         self._calls: Dict[int, Tuple[list, list, list]] = {}
@@ -81,6 +86,7 @@ class Engine:
         # BN statistics and the head stay fp32 master copies either way)
         at = torch.bfloat16 if self.dt == _ffi.JR_BF16 else fl
         self.act_dtype = at
+        self.esz = 2 if self.dt == _ffi.JR_BF16 else 4
         # the image buffer is kept one 16 B DMA piece wide per pixel (4 fp32 /
         # 8 bf16 channels, zeros past c = 3): conv1's c_in = 3 runs on libjr's
         # virtual channel padding
@@ -88,14 +94,22 @@ class Engine:
         self.in_stride = (g.bufs[g.input_buf].c + q - 1) // q * q
         self.acts = [self._t(B * b.h * b.w * (self.in_stride if b.id == g.input_buf else b.c), at)
                      for b in g.bufs]
-        self.raw = {n.idx: self._t(B * n.ho * n.wo * n.cout, at) for n in g.convs}
-        self.stats = self._t(2 * sum(n.cout for n in g.convs))
-        self.mean, self.invstd = {}, {}
+        # raw (pre-BN) output and BN statistics per conv launch; a fused
+        # group's members see channel slices of them
+        self.raw_unit = {u.first.idx: self._t(B * u.ho * u.wo * u.cout, at) for u in self.cunits}
+        self.stats = self._t(2 * sum(u.cout for u in self.cunits))
+        self.raw, self.mean, self.invstd = {}, {}, {}
+        self.mean_unit, self.invstd_unit = {}, {}
         off = 0
-        for n in g.convs:
-            self.mean[n.idx] = self.stats[off:off + n.cout]
-            self.invstd[n.idx] = self.stats[off + n.cout:off + 2 * n.cout]
-            off += 2 * n.cout
+        for u in self.cunits:
+            r = self.raw_unit[u.first.idx].view(B * u.ho * u.wo, u.cout)
+            self.mean_unit[u.first.idx] = self.stats[off:off + u.cout]
+            self.invstd_unit[u.first.idx] = self.stats[off + u.cout:off + 2 * u.cout]
+            for n, co in zip(u.members, u.col_off):
+                self.raw[n.idx] = r[:, co:co + n.cout]
+                self.mean[n.idx] = self.stats[off + co:off + co + n.cout]
+                self.invstd[n.idx] = self.stats[off + u.cout + co:off + u.cout + co + n.cout]
+            off += 2 * u.cout
         self.argmax = {}
         for i, n in enumerate(g.nodes):
             if n.kind == "maxpool":
@@ -112,37 +126,38 @@ class Engine:
             self.accum = self._t(self.nparam)
             self.dacts = [self._t(B * b.h * b.w * b.c, at) if b.id != g.input_buf else None
                           for b in g.bufs]
-            self.draw = self._t(max(B * n.ho * n.wo * n.cout for n in g.convs), at)
+            self.draw = self._t(max(B * u.ho * u.wo * u.cout for u in self.cunits), at)
             self.dfeat = self._t(B * feat_c)
         if self.dt == _ffi.JR_BF16:
             self._alloc_bf16_filters()
         ws = 0
-        for n in g.convs:
-            d = self._conv_desc(n, B)
+        for u in self.cunits:
+            d = self._conv_desc(u, B)
             ops = (_ffi.JR_CONV_FWD, _ffi.JR_CONV_BWD_DATA, _ffi.JR_CONV_BWD_FILTER)
             for op in (ops if self.train_mode else ops[:1]):
                 ws = max(ws, self.lib.jr_conv2d_workspace_size(ctypes.byref(d), op, self.dt))
-            ws = max(ws, self.lib.jr_bn_workspace_size(B * n.ho * n.wo, n.cout))
+            for n in u.members:
+                ws = max(ws, self.lib.jr_bn_workspace_size(B * n.ho * n.wo, n.cout))
         self.ws_bytes = int(ws)
         self.ws = self._t((self.ws_bytes + 15) // 4 + 4)
 
     def _alloc_bf16_filters(self) -> None:
-        """bf16 operand copies of every conv kernel, refreshed from the fp32
-        master parameters by ONE jr_conv_weights_bf16_multi launch at the
-        start of each forward: HWIO (bwd_data) and W^T [co][kh][kw][c8] (fwd)."""
+        """bf16 operand copies of every conv launch's kernel (block), refreshed
+        from the fp32 master parameters by ONE jr_conv_weights_bf16_multi
+        launch at the start of each forward: HWIO (bwd_data) and
+        W^T [co][kh][kw][c8] (fwd)."""
         L = self.lib
         layers, tiles = [], 0
         self.wb_hwio_off, self.wb_t_off = {}, {}
         ho = to = 0
-        for n in self.g.convs:
-            src, _ = self.poffs[f"{n.name}/kernel"]
-            c8 = (n.cin + 7) // 8 * 8
-            layers.append(_ffi.WPrep(src, ho, to, n.kh, n.kw, n.cin, n.cout, tiles, 0))
-            self.wb_hwio_off[n.idx], self.wb_t_off[n.idx] = ho, to
-            tiles += L.jr_conv_weights_bf16_tiles(n.kh, n.kw, n.cin, n.cout)
+        for u in self.cunits:
+            c8 = (u.cin + 7) // 8 * 8
+            layers.append(_ffi.WPrep(u.koff, ho, to, u.kh, u.kw, u.cin, u.cout, tiles, 0))
+            self.wb_hwio_off[u.first.idx], self.wb_t_off[u.first.idx] = ho, to
+            tiles += L.jr_conv_weights_bf16_tiles(u.kh, u.kw, u.cin, u.cout)
             # 16 B-aligned starts (8 bf16)
-            ho += (n.kh * n.kw * n.cin * n.cout + 7) // 8 * 8
-            to += n.cout * n.kh * n.kw * c8
+            ho += (u.kh * u.kw * u.cin * u.cout + 7) // 8 * 8
+            to += u.cout * u.kh * u.kw * c8
         arr = (_ffi.WPrep * len(layers))(*layers)
         self.wprep_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
         self.wprep_layers, self.wprep_tiles = len(layers), tiles
@@ -154,87 +169,89 @@ class Engine:
                 (self.wprep_table.data_ptr(), self.wprep_layers, self.wprep_tiles, self.params.data_ptr(),
                  self.w_hwio.data_ptr(), self.w_t.data_ptr(), self._s), "wprep_bf16")
 
-    def _wf(self, n: ConvNode) -> int:
-        """Filter operand of conv fwd: fp32 HWIO master, or the bf16 W^T copy."""
+    def _wf(self, u: ConvUnit) -> int:
+        """Filter operand of conv fwd: fp32 HWIO master block, or its bf16 W^T copy."""
         if self.dt == _ffi.JR_BF16:
-            return self.w_t.data_ptr() + 2 * self.wb_t_off[n.idx]
-        return self._p(f"{n.name}/kernel")
+            return self.w_t.data_ptr() + 2 * self.wb_t_off[u.first.idx]
+        return self.params.data_ptr() + 4 * u.koff
 
-    def _wd(self, n: ConvNode) -> int:
-        """Filter operand of conv bwd_data: fp32 HWIO master, or its bf16 copy."""
+    def _wd(self, u: ConvUnit) -> int:
+        """Filter operand of conv bwd_data: fp32 HWIO master block, or its bf16 copy."""
         if self.dt == _ffi.JR_BF16:
-            return self.w_hwio.data_ptr() + 2 * self.wb_hwio_off[n.idx]
-        return self._p(f"{n.name}/kernel")
+            return self.w_hwio.data_ptr() + 2 * self.wb_hwio_off[u.first.idx]
+        return self.params.data_ptr() + 4 * u.koff
 
     def autotune(self) -> None:
-        """jr_conv2d_autotune every conv op of the planned batch (cudnnFind
+        """jr_conv2d_autotune every conv launch of the planned batch (cudnnFind
         style: times each tile configuration on this engine's own buffers and
-        caches the fastest in libjr).  Runs before any data is loaded:
-        it overwrites raw / gradient buffers."""
+        caches the fastest in libjr).  Runs before any data is loaded: it
+        overwrites raw / gradient buffers."""
         L, B = self.lib, self.batch
         ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
         s = self._s
         if self.dt == _ffi.JR_BF16:
             fn, args, name = self._wprep_call()
             _ffi.check(name, fn(*args))
-        for n in self.g.convs:
-            d = self._conv_desc(n, B)
-            x = self.acts[n.x].data_ptr()
-            w = self._wf(n)
-            _ffi.check("autotune fwd", L.jr_conv2d_autotune(ctypes.byref(d), _ffi.JR_CONV_FWD, self.dt, x, w,
-                                                             self.raw[n.idx].data_ptr(), ws, wsb, s))
+        for u in self.cunits:
+            d = self._conv_desc(u, B)
+            x = self.acts[u.x].data_ptr()
+            raw = self.raw_unit[u.first.idx].data_ptr()
+            _ffi.check("autotune fwd", L.jr_conv2d_autotune(ctypes.byref(d), _ffi.JR_CONV_FWD, self.dt, x,
+                                                             self._wf(u), raw, ws, wsb, s))
             if not self.train_mode:
                 continue
             _ffi.check("autotune wgrad", L.jr_conv2d_autotune(
                 ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, self.dt, x, self.draw.data_ptr(),
-                self._gp(f"{n.name}/kernel"), ws, wsb, s))
-            if n.x != self.g.input_buf:
+                self.grads.data_ptr() + 4 * u.koff, ws, wsb, s))
+            if u.x != self.g.input_buf:
                 _ffi.check("autotune dgrad", L.jr_conv2d_autotune(
-                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.dt, self.draw.data_ptr(), self._wd(n),
-                    self.dacts[n.x].data_ptr(), ws, wsb, s))
+                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.dt, self.draw.data_ptr(), self._wd(u),
+                    self.dacts[u.x].data_ptr(), ws, wsb, s))
         self.synchronize()
         if self.train_mode:
             self.grads.zero_()
 
     def conv_configs(self) -> dict:
-        """{conv name: (fwd cfg, wgrad cfg, [dgrad cfg per phase])} in use."""
+        """{conv launch name: (fwd cfg, wgrad cfg, [dgrad cfg per phase])} in use."""
         out = {}
-        for n in self.g.convs:
-            d = self._conv_desc(n, self.batch)
+        for u in self.cunits:
+            d = self._conv_desc(u, self.batch)
             f = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_FWD, self.dt, 0)
             wg = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, self.dt, 0)
             dg = [self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.dt, p)
-                  for p in range(n.stride * n.stride)]
-            out[n.name] = (f, wg, dg)
+                  for p in range(u.stride * u.stride)]
+            out[u.name] = (f, wg, dg)
         return out
 
     # ------------------------------------------------------------ parameters
     def load_params(self, flat: np.ndarray) -> None:
-        flat = np.ascontiguousarray(flat, dtype=np.float32)
-        if flat.size != self.nparam:
-            raise ValueError(f"expected {self.nparam} parameters, got {flat.size}")
-        self.params.copy_(torch.from_numpy(flat).to(self.device))
+        """Keras-layout flat parameters (jr.init.param_layout order)."""
+        self.params.copy_(torch.from_numpy(self.plan.to_internal(self.g, flat)).to(self.device))
         if self.train_mode:
             self.accum.zero_()
             self.grads.zero_()
 
     def params_numpy(self) -> np.ndarray:
+        """Parameters in the Keras layout (checkpoints, the oracle)."""
         torch.cuda.synchronize(self.device)
-        return self.params.cpu().numpy()
+        return self.plan.to_keras(self.g, self.params.cpu().numpy())
+
+    def grads_numpy(self) -> np.ndarray:
+        """Gradients of the last backward in the Keras layout."""
+        torch.cuda.synchronize(self.device)
+        return self.plan.to_keras(self.g, self.grads.cpu().numpy())
 
     def _p(self, name: str) -> int:
-        off, _ = self.poffs[name]
-        return self.params.data_ptr() + 4 * off
+        return self.params.data_ptr() + 4 * self.plan.poff[name]
 
     def _gp(self, name: str) -> int:
-        off, _ = self.poffs[name]
-        return self.grads.data_ptr() + 4 * off
+        return self.grads.data_ptr() + 4 * self.plan.poff[name]
 
     # ------------------------------------------------------------ descriptors
-    def _conv_desc(self, n: ConvNode, B: int) -> _ffi.ConvDesc:
-        xs = self.in_stride if n.x == self.g.input_buf else n.cin
-        return _ffi.ConvDesc(B, n.h, n.w, n.cin, n.cout, n.kh, n.kw, n.stride, n.stride,
-                             n.pad_h, n.pad_w, n.ho, n.wo, 0, xs, 0, n.cout)
+    def _conv_desc(self, u: ConvUnit, B: int) -> _ffi.ConvDesc:
+        xs = self.in_stride if u.x == self.g.input_buf else u.cin
+        return _ffi.ConvDesc(B, u.h, u.w, u.cin, u.cout, u.kh, u.kw, u.stride, u.stride,
+                             u.pad_h, u.pad_w, u.ho, u.wo, 0, xs, 0, u.cout)
 
     def _pool_desc(self, n: PoolNode, B: int) -> _ffi.PoolDesc:
         yb = self.g.bufs[n.y.buf]
@@ -252,23 +269,29 @@ class Engine:
         keep = []  # keep ctypes structs alive
         fwd, bwd, opt = [], [], []
         A = lambda bid: self.acts[bid].data_ptr()  # noqa: E731
+        unit_of = self.plan.unit_of
         if dt == _ffi.JR_BF16:
             fwd.append(self._wprep_call())
         for i, n in enumerate(g.nodes):
             if n.kind == "conv":
-                d = self._conv_desc(n, B)
+                u = unit_of[n.idx]
+                if u.first is not n:
+                    continue            # emitted with the group's first member
+                d = self._conv_desc(u, B)
                 keep.append(d)
-                M = B * n.ho * n.wo
-                yb = g.bufs[n.y.buf]
-                fwd.append((L.jr_conv2d_fwd, (ctypes.byref(d), dt, A(n.x), self._wf(n),
-                                              self.raw[n.idx].data_ptr(), ws, wsb, s), "conv_fwd"))
-                fwd.append((L.jr_bn_stats, (dt, self.raw[n.idx].data_ptr(), M, n.cout, BN_EPS,
-                                            self.mean[n.idx].data_ptr(), self.invstd[n.idx].data_ptr(),
-                                            ws, wsb, s), "bn_stats"))
-                fwd.append((L.jr_bn_relu_apply, (dt, self.raw[n.idx].data_ptr(), M, n.cout,
-                                                 self.mean[n.idx].data_ptr(), self.invstd[n.idx].data_ptr(),
-                                                 self._p(f"batch_normalization_{n.idx + 1}/beta"),
-                                                 A(n.y.buf), n.y.c_off, yb.c, s), "bn_relu"))
+                M = B * u.ho * u.wo
+                raw = self.raw_unit[u.first.idx].data_ptr()
+                # conv + the BN batch statistics of its raw output, fused
+                fwd.append((L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), dt, A(u.x), self._wf(u), raw, BN_EPS,
+                                                       self.mean_unit[u.first.idx].data_ptr(),
+                                                       self.invstd_unit[u.first.idx].data_ptr(), ws, wsb, s),
+                            "conv_fwd"))
+                for m, co in zip(u.members, u.col_off):
+                    yb = g.bufs[m.y.buf]
+                    fwd.append((L.jr_bn_relu_apply, (dt, raw, co, u.cout, M, m.cout, self.mean[m.idx].data_ptr(),
+                                                     self.invstd[m.idx].data_ptr(),
+                                                     self._p(f"batch_normalization_{m.idx + 1}/beta"),
+                                                     A(m.y.buf), m.y.c_off, yb.c, s), "bn_relu"))
             elif n.kind == "maxpool":
                 d = self._pool_desc(n, B)
                 keep.append(d)
@@ -297,27 +320,31 @@ class Engine:
             written = set()
             for i in range(len(g.nodes) - 1, -1, -1):
                 n = g.nodes[i]
-                yb = g.bufs[n.y.buf]
                 acc = 1 if n.x in written else 0
                 if n.kind == "conv":
-                    d = self._conv_desc(n, B)
+                    u = unit_of[n.idx]
+                    if u.first is not n:
+                        continue        # a group runs at its first member: every member's dy is final then
+                    d = self._conv_desc(u, B)
                     keep.append(d)
-                    M = B * n.ho * n.wo
-                    bwd.append((L.jr_bn_relu_bwd, (dt, D(n.y.buf), n.y.c_off, yb.c, self.raw[n.idx].data_ptr(),
-                                                   M, n.cout, self.mean[n.idx].data_ptr(),
-                                                   self.invstd[n.idx].data_ptr(),
-                                                   self._p(f"batch_normalization_{n.idx + 1}/beta"),
-                                                   self.draw.data_ptr(),
-                                                   self._gp(f"batch_normalization_{n.idx + 1}/beta"),
-                                                   ws, wsb, s), "bn_relu_bwd"))
-                    bwd.append((L.jr_conv2d_bwd_filter, (ctypes.byref(d), dt, A(n.x), self.draw.data_ptr(),
-                                                         self._gp(f"{n.name}/kernel"), ws, wsb, s), "conv_wgrad"))
-                    if n.x != g.input_buf:
+                    M = B * u.ho * u.wo
+                    raw = self.raw_unit[u.first.idx].data_ptr()
+                    for m, co in zip(u.members, u.col_off):
+                        yb = g.bufs[m.y.buf]
+                        bwd.append((L.jr_bn_relu_bwd, (dt, D(m.y.buf), m.y.c_off, yb.c, raw, co, u.cout, M, m.cout,
+                                                       self.mean[m.idx].data_ptr(), self.invstd[m.idx].data_ptr(),
+                                                       self._p(f"batch_normalization_{m.idx + 1}/beta"),
+                                                       self.draw.data_ptr(),
+                                                       self._gp(f"batch_normalization_{m.idx + 1}/beta"),
+                                                       ws, wsb, s), "bn_relu_bwd"))
+                    bwd.append((L.jr_conv2d_bwd_filter, (ctypes.byref(d), dt, A(u.x), self.draw.data_ptr(),
+                                                         self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
+                                "conv_wgrad"))
+                    if u.x != g.input_buf:
                         bwd.append((L.jr_conv2d_bwd_data, (ctypes.byref(d), dt, self.draw.data_ptr(),
-                                                           self._wd(n), D(n.x), acc, ws, wsb, s),
-                                    "conv_dgrad"))
-                        written.add(n.x)
-                    bwd.append(("param_ready", self.poffs[f"{n.name}/kernel"][0], "hook"))
+                                                           self._wd(u), D(u.x), acc, ws, wsb, s), "conv_dgrad"))
+                        written.add(u.x)
+                    bwd.append(("param_ready", u.koff, "hook"))
                 elif n.kind == "maxpool":
                     d = self._pool_desc(n, B)
                     keep.append(d)

@@ -43,7 +43,8 @@ def test_validation_errors_without_gpu():
     d = _ffi.ConvDesc(1, 8, 8, 16, 24, 3, 3, 1, 1, 1, 1, 8, 8, 0, 16, 0, 24)
     assert L.jr_conv2d_fwd(ctypes.byref(d), 0, 16, 16, 16, None, 0, None) == -3   # c_out % 16
     assert L.jr_conv2d_workspace_size(None, 0, 0) == 0
-    assert L.jr_bn_relu_apply(0, 16, 10, 6, 16, 16, 16, 16, 0, 6, None) == -1      # c % 4
+    assert L.jr_bn_relu_apply(0, 16, 0, 6, 10, 6, 16, 16, 16, 16, 0, 6, None) == -1   # c % 4
+    assert L.jr_bn_relu_apply(0, 16, 4, 8, 10, 8, 16, 16, 16, 16, 0, 8, None) == -1   # x slice out of range
     assert L.jr_head_fwd(0, None, None, None, None, 1, 1, 1, None, None, None, None) == -1
     assert L.jr_graph_launch(None, None) == -1
 

@@ -52,7 +52,7 @@ def test_forward_and_one_step_match_oracle(res, batch):
 
     eng.backward()
     eng.synchronize()
-    G = unflatten(eng.g, eng.grads.cpu().numpy())
+    G = unflatten(eng.g, eng.grads_numpy())
     e_gpu = _grad_errors(G, grads_ref)
     e_cpu = _grad_errors(grads_32, grads_ref)
     # A ReLU whose pre-activation lies within fp32 rounding of 0 may flip
@@ -114,28 +114,33 @@ def test_bf16_loss_curve_tracks_f32():
     """bf16 path (BASELINE configs 3 and 5): bf16 activations / filter copies,
     fp32 MFMA accumulation, fp32 master weights, BN statistics, head and
     optimizer.  Per-op parity is pinned teacher-forced in
-    test_gpu_layerwise.py; end to end, a bf16 forward differs from fp64 by
-    far more than one rounding (this BN-heavy net amplifies a 2^-9 input
-    perturbation ~10^3-fold at small batches), so the end-to-end bar is the
-    training trajectory: 40 Nesterov steps over a fixed stream of distinct
-    synthetic batches, bf16 vs the fp32 engine from the same weights, 10-step
-    window means of the loss within 0.05 (+5 % of the fp32 value)."""
+    test_gpu_layerwise.py; end to end a bf16 forward differs from fp32 by far
+    more than one rounding (this BN-heavy net amplifies a 2^-9 perturbation
+    up to ~10^3-fold at small BN populations; on random labels two fp32
+    implementations decorrelate within a few steps too), so the end-to-end
+    bar is the shape of the training trajectory at the full 299^2 geometry:
+    30 Nesterov steps on one fixed batch of 8 from the same weights, bf16 vs
+    the fp32 engine: step-0 loss within 0.05, both fit the batch (final loss
+    < 0.5x initial), mean |loss difference| over the curve <= 0.1."""
     from jr.engine import Engine
     from jr import synth
-    B, res = 8, 139
+    B, res = 8, 299
+    imgs = synth.fundus_batch(0, B, res)
+    y = np.array([[1.0], [0.0]] * 4, np.float32)
     eng = {dt: Engine(B, res, res, seed=5, dtype=dt) for dt in ("f32", "bf16")}
     curves = {dt: [] for dt in eng}
-    for step in range(40):
-        imgs = synth.fundus_batch(step * B, B, res)
-        y = synth.labels(step * B, B)
-        for dt, e in eng.items():
-            e.set_batch(imgs, y)
+    for dt, e in eng.items():
+        e.set_batch(imgs, y)
+        for _ in range(30):
             e.train_step()
             curves[dt].append(e.loss_value())
     f, h = np.array(curves["f32"]), np.array(curves["bf16"])
+    print("f32 ", np.round(f, 3))
+    print("bf16", np.round(h, 3))
     assert np.all(np.isfinite(h))
-    wf, wh = f.reshape(4, 10).mean(1), h.reshape(4, 10).mean(1)
-    assert np.all(np.abs(wf - wh) <= 0.05 + 0.05 * np.abs(wf)), (wf, wh)
+    assert abs(f[0] - h[0]) <= 0.05, (f[0], h[0])
+    assert f[-3:].mean() < 0.5 * f[0] and h[-3:].mean() < 0.5 * h[0], (f, h)
+    assert np.mean(np.abs(f - h)) <= 0.1, (f, h)
 
 
 def test_bf16_graph_replay_and_training_descends():
@@ -160,3 +165,29 @@ def test_bf16_graph_replay_and_training_descends():
     assert a.loss_value() == b.loss_value()
     assert np.all(np.isfinite(losses))
     assert np.mean(losses[-3:]) < 0.5 * losses[0], losses
+
+
+@pytest.mark.parametrize("dtype", ["f32"])
+def test_sibling_fusion_matches_unfused(dtype):
+    """Fused sibling 1x1 launches (jr.plan) compute the same step as one
+    launch per layer: same logits/loss within one-op rounding (the GEMM tiles
+    differ, so the fp32 summation order may), same Keras-layout gradients.
+    (bf16 fusion is pinned per op in test_gpu_layerwise.py: end to end, bf16
+    rounding differences are amplified beyond any useful bound.)"""
+    from jr.engine import Engine
+    from jr import synth
+    imgs = synth.fundus_batch(7, 4, 107)
+    y = np.array([[1.0], [0.0], [1.0], [0.0]], np.float32)
+    e = {f: Engine(4, 107, 107, seed=9, dtype=dtype, fuse_siblings=f) for f in (True, False)}
+    for x in e.values():
+        x.set_batch(imgs, y)
+        x.forward()
+        x.backward()
+        x.synchronize()
+    la, lb = e[True].logits.cpu().numpy(), e[False].logits.cpu().numpy()
+    tol = 1e-4 if dtype == "f32" else 5e-2
+    assert np.max(np.abs(la - lb)) <= tol * max(1.0, np.abs(lb).max()), (la, lb)
+    ga, gb = e[True].grads_numpy(), e[False].grads_numpy()
+    cos = float(ga @ gb / (np.linalg.norm(ga) * np.linalg.norm(gb)))
+    assert cos >= (0.9999 if dtype == "f32" else 0.98), cos
+    assert np.array_equal(e[True].params_numpy(), e[False].params_numpy())

@@ -68,7 +68,7 @@ def test_every_layer_teacher_forced(dtype, res, batch):
     eng.synchronize()
     g, B = eng.g, batch
     P = unflatten(g, eng.params_numpy())
-    G = unflatten(g, eng.grads.cpu().numpy())
+    G = unflatten(g, eng.grads_numpy())
     rnd = _bf16 if dtype == "bf16" else (lambda a: np.asarray(a, np.float64))
 
     def buf(bid, dacts=False):

@@ -212,22 +212,28 @@ def test_bn_relu_fwd_bwd(m, c):
                                      ws.data_ptr(), wsb, None))
     assert relerr(host(MEAN), mean_ref) < 1e-6
     assert relerr(host(INV), inv_ref) < 1e-6
-    # write into a channel slice of a wider buffer
+    # read x as channel slice [4, 4 + c) of a wider raw buffer (a fused
+    # sibling-conv group) and write into a channel slice of a wider output
+    XW = np.zeros((m, c + 12), np.float32)
+    XW[:, 4:4 + c] = x
+    XS = dev(XW)
     Y = torch.zeros(m * (c + 16), device="cuda")
-    ffi.check("apply", L.jr_bn_relu_apply(0, X.data_ptr(), m, c, MEAN.data_ptr(), INV.data_ptr(), BETA.data_ptr(),
-                                          Y.data_ptr(), 16, c + 16, None))
+    ffi.check("apply", L.jr_bn_relu_apply(0, XS.data_ptr(), 4, c + 12, m, c, MEAN.data_ptr(), INV.data_ptr(),
+                                          BETA.data_ptr(), Y.data_ptr(), 16, c + 16, None))
     got = host(Y).reshape(m, c + 16)
     assert np.max(np.abs(got[:, 16:] - y_ref)) < 2e-5 * max(1.0, np.abs(y_ref).max())
     assert np.all(got[:, :16] == 0)
     dx_ref, db_ref = R.bn_relu_bwd(dy, x, beta, mask=got[:, 16:] > 0)
     DYb = np.zeros((m, c + 8), np.float32)
     DYb[:, 8:] = dy
-    DX, DB = torch.zeros(m * c, device="cuda"), torch.zeros(c, device="cuda")
-    ffi.check("bwd", L.jr_bn_relu_bwd(0, dev(DYb).data_ptr(), 8, c + 8, X.data_ptr(), m, c, MEAN.data_ptr(),
-                                      INV.data_ptr(), BETA.data_ptr(), DX.data_ptr(), DB.data_ptr(), ws.data_ptr(),
-                                      wsb, None))
+    DX, DB = torch.full((m * (c + 12),), 7.0, device="cuda"), torch.zeros(c, device="cuda")
+    ffi.check("bwd", L.jr_bn_relu_bwd(0, dev(DYb).data_ptr(), 8, c + 8, XS.data_ptr(), 4, c + 12, m, c,
+                                      MEAN.data_ptr(), INV.data_ptr(), BETA.data_ptr(), DX.data_ptr(), DB.data_ptr(),
+                                      ws.data_ptr(), wsb, None))
+    dxg = host(DX).reshape(m, c + 12)
+    assert np.all(dxg[:, :4] == 7.0) and np.all(dxg[:, 4 + c:] == 7.0)   # only the slice is written
     assert relerr(host(DB), db_ref) < 1e-5
-    assert relerr(host(DX).reshape(m, c), dx_ref) < 1e-4
+    assert relerr(dxg[:, 4:4 + c], dx_ref) < 1e-4
 
 
 @pytest.mark.parametrize("shape", [(2, 147, 147, 64), (2, 35, 35, 288), (3, 17, 17, 768), (1, 9, 10, 8)])
