@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--res", type=int, default=299)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a HIP graph")
+    ap.add_argument("--lanes", type=int, default=2, help="streams for branch-level concurrency (jr.lanes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=64)
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -56,7 +57,7 @@ def conv_roofline(eng, steps: int = 3):
     """Instrumented eager pass: HIP events (torch.cuda.Event on eng.stream)
     bracket every conv fwd/dgrad/wgrad call; returns (flops/step, conv s/step)."""
     from jr import _ffi
-    fwd, bwd, opt, _ = eng._build_calls(eng.batch)
+    fwd, bwd, opt, _, _ = eng._build_calls(eng.batch, 1)     # one lane: calls do not overlap
     conv_names = {"conv_fwd", "conv_dgrad", "conv_wgrad"}
     flops = 0
     for n in eng.g.convs:
@@ -65,23 +66,42 @@ def conv_roofline(eng, steps: int = 3):
     pairs = []
     for _ in range(steps):
         for calls in (fwd, bwd, opt):
-            for fn, args, name in calls:
-                if fn == "param_ready":
+            for c in calls:
+                if c.fn == "param_ready":
                     continue
-                if name in conv_names:
+                if c.name in conv_names:
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
                     e0.record(eng.stream)
-                    rc = fn(*args)
+                    rc = c.fn(*c.args)
                     e1.record(eng.stream)
                     pairs.append((e0, e1))
                 else:
-                    rc = fn(*args)
+                    rc = c.fn(*c.args)
                 if rc:
-                    raise _ffi.JRError(name, rc, _ffi.last_error())
+                    raise _ffi.JRError(c.name, rc, _ffi.last_error())
     eng.synchronize()
     t = sum(a.elapsed_time(b) for a, b in pairs) / 1e3 / steps
     return flops, t, len(pairs) // steps
+
+
+def pmc_traffic(dtype: str, B: int, res: int) -> dict:
+    """HBM bytes of the conv family per training step from the committed
+    rocprofv3 PMC summary of the same workload (tools/pmc_step.sh ->
+    profiles/r01_pmc_<dtype>.json: FETCH_SIZE x 2 (gfx950 tallies 128-B
+    requests at 64 B, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, over the
+    conv GEMM, split-K reduce and statistics kernels of one step).  bench.py
+    cannot run the profiler itself, so `traffic` is null without that file."""
+    if (B, res) != (64, 299):
+        return {}
+    p = os.path.join(ROOT, "profiles", f"r01_pmc_{dtype}.json")
+    if not os.path.exists(p):
+        return {}
+    fam = json.load(open(p))["families"].get("conv", {})
+    if "hbm_read_bytes" not in fam or "hbm_write_bytes" not in fam:
+        return {}
+    return {"traffic": round(fam["hbm_read_bytes"] + fam["hbm_write_bytes"]),
+            "traffic_unit": "HBM bytes per step (conv family, PMC)", "traffic_source": os.path.relpath(p, ROOT)}
 
 
 def cpu_baseline(args, res):
@@ -127,7 +147,7 @@ def main():
     from jr.dist import BucketAllReduce
 
     B, res = args.batch, args.res
-    eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0)
+    eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0, lanes=args.lanes)
     imgs = synth.fundus_batch(rank * B, B, res)
     labels = synth.labels(rank * B, B)
     eng.set_batch(imgs, labels)
@@ -184,6 +204,7 @@ def main():
                     "kernel": f"conv implicit-GEMM fwd+dgrad+wgrad ({nconv} calls/step)",
                     "conv_ms_per_step": round(tconv * 1e3, 3),
                     "algorithmic_gflop_per_step": round(flops / 1e9, 1)}
+            roof.update(pmc_traffic(args.dtype, B, res))
         out = {
             "metric": "train images/sec, Inception-v3 299^2 bs64/GPU",
             "value": round(imgs_s, 2), "unit": "images/sec", "n_gpus": world,
@@ -192,7 +213,7 @@ def main():
             "dtype": args.dtype, "data": "synthetic fundus-shaped uint8 299x299x3 (jr.synth), random Keras init",
             "config": {"workload": f"Inception-v3 {res}x{res} {args.dtype} training, batch {B}/GPU, "
                                    f"Nesterov lr 3e-3 m 0.9", "model": "inception_v3", "global_batch": B * world,
-                       "seq_len": None, "parallelism": f"dp{world}", "hip_graph": use_graph},
+                       "seq_len": None, "parallelism": f"dp{world}", "hip_graph": use_graph, "lanes": args.lanes},
             "final_loss": round(loss, 5),
             "roofline": roof,
         }

@@ -561,10 +561,13 @@ static void stats_geom(int dtype, const Plan& p, int* P, int* R) {
 
 static size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
+constexpr int kStatsChunk = 4096;   // partials one finalize block combines
+
 static size_t stats_ws(int dtype, const Plan& p) {
   int P, R;
   stats_geom(dtype, p, &P, &R);
-  return 2 * (size_t)p.N * P * sizeof(float);
+  const size_t S = P > kStatsChunk ? (size_t)ceil_div(P, kStatsChunk) : 0;
+  return (2 * (size_t)p.N * P + 3 * (size_t)p.N * S) * sizeof(float);
 }
 
 // Fast-path kernels (UT): FWD/DGRAD when the reduction channel radix is a
@@ -687,8 +690,20 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
       rc = check_launch("conv split-k reduce + stats");
       if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_stats_finalize, dim3(p.N), dim3(256), 0, s, (const float*)a.stats, sP, sR, p.M, p.N,
-                       st->eps, st->mean, st->invstd);
+    if (sP <= kStatsChunk) {
+      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N), dim3(256), 0, s, (const float*)a.stats, (const float*)nullptr,
+                         sP, sR, p.M, p.N, sP, st->eps, st->mean, st->invstd, (float*)nullptr);
+    } else {   // two stages: per-chunk (mean, M2, n), then the final combine
+      const int S = (int)ceil_div(sP, kStatsChunk);
+      float* s2 = a.stats + 2 * (size_t)p.N * sP;
+      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N, S), dim3(256), 0, s, (const float*)a.stats, (const float*)nullptr,
+                         sP, sR, p.M, p.N, kStatsChunk, st->eps, (float*)nullptr, (float*)nullptr, s2);
+      rc = check_launch("conv stats combine");
+      if (rc) return rc;
+      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N), dim3(256), 0, s, (const float*)s2,
+                         (const float*)(s2 + 2 * (size_t)p.N * S), S, 0, p.M, p.N, S, st->eps, st->mean, st->invstd,
+                         (float*)nullptr);
+    }
     return check_launch("conv stats finalize");
   }
   if (p.splits <= 1) return rc;
@@ -857,48 +872,65 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
   return rc;
 }
 
-__global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict__ part, int P, int R, int M, int N,
-                                                        float eps, float* mean, float* invstd) {
-  __shared__ double red[256];
+// Combine statistics partials in ONE pass (each is a round trip to memory
+// the writer XCDs flushed): with the shift K = mean of partial 0,
+//   mu = K + sum n_i d_i / M,  M2 = sum M2_i + sum n_i d_i^2 - M (mu - K)^2,
+// d_i = mean_i - K, in fp64, fixed-shape tree: deterministic.  Partial
+// counts are n_i = clamp(M - i R, 0, R), or explicit (cnt != nullptr, from
+// the first stage of a two-stage combine).  Block (n, s) combines partials
+// [s*chunk, (s+1)*chunk) of channel n; with gridDim.y == 1 it finalizes
+// (mean, invstd), else it writes one (mean, M2, count) partial per chunk.
+__global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict__ part, const float* __restrict__ cnt,
+                                                        int P, int R, int M, int N, int chunk, float eps,
+                                                        float* mean, float* invstd, float* out) {
+  __shared__ double red[3][256];
   const int n = blockIdx.x, t = threadIdx.x;
   const float* pm = part + (long long)n * P;
   const float* pq = part + (long long)(N + n) * P;
-  auto cnt = [&](int i) { return (double)min(max(M - i * R, 0), R); };
-  auto tree = [&](double v) {
-    red[t] = v;
-    __syncthreads();
-    for (int h = 128; h > 0; h >>= 1) {
-      if (t < h) red[t] += red[t + h];
-      __syncthreads();
-    }
-    const double r = red[0];
-    __syncthreads();
-    return r;
-  };
-  double a[4] = {0, 0, 0, 0};
-  for (int i0 = 0; i0 < P; i0 += 1024) {
+  const float* pc = cnt ? cnt + (long long)n * P : nullptr;
+  const int i0 = blockIdx.y * chunk, i1 = min(P, i0 + chunk);
+  const double K = pm[i0];
+  double sn = 0, sd = 0, sq = 0;
+  for (int b = i0; b < i1; b += 256 * 8) {
+    float vm[8], vq[8], vc[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u * 256 + t;
-      if (i < P) a[u] += cnt(i) * (double)pm[i];
+    for (int u = 0; u < 8; ++u) {
+      const int i = b + u * 256 + t;
+      const bool ok = i < i1;
+      vm[u] = ok ? pm[i] : 0.f;
+      vq[u] = ok ? pq[i] : 0.f;
+      vc[u] = !ok ? 0.f : (pc ? pc[i] : (float)min(max(M - i * R, 0), R));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double d = (double)vm[u] - K, c = vc[u];
+      sn += c;
+      sd += c * d;
+      sq += (double)vq[u] + c * d * d;
     }
   }
-  const double mu = tree((a[0] + a[1]) + (a[2] + a[3])) / (double)M;
-  double b[4] = {0, 0, 0, 0};
-  for (int i0 = 0; i0 < P; i0 += 1024) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u * 256 + t;
-      if (i < P) {
-        const double d = (double)pm[i] - mu;
-        b[u] += (double)pq[i] + cnt(i) * d * d;
-      }
+  red[0][t] = sn; red[1][t] = sd; red[2][t] = sq;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (t < h) {
+      red[0][t] += red[0][t + h];
+      red[1][t] += red[1][t + h];
+      red[2][t] += red[2][t + h];
     }
+    __syncthreads();
   }
-  const double m2 = tree((b[0] + b[1]) + (b[2] + b[3]));
-  if (t == 0) {
-    mean[n] = (float)mu;
+  if (t != 0) return;
+  const double tn = red[0][0];
+  const double dm = tn > 0 ? red[1][0] / tn : 0.0;
+  const double m2 = fmax(red[2][0] - tn * dm * dm, 0.0);
+  if (gridDim.y == 1) {
+    mean[n] = (float)(K + dm);
     invstd[n] = (float)(1.0 / sqrt(m2 / (double)M + (double)eps));
+  } else {
+    const int S = gridDim.y;
+    out[(long long)n * S + blockIdx.y] = (float)(K + dm);
+    out[(long long)(N + n) * S + blockIdx.y] = (float)m2;
+    out[(long long)(2 * N + n) * S + blockIdx.y] = (float)tn;
   }
 }
 

@@ -378,11 +378,11 @@ __global__ void __launch_bounds__(256) k_splitk_reduce_stats(const float* __rest
 }
 
 // (mean, invstd) per channel from stats[2][N][P] partials of R rows each
-// (the last ones hold fewer, down to 0): mean = sum n_i mean_i / M, then
-// M2 = sum M2_i + n_i (mean_i - mean)^2, both in fp64 with a fixed-shape
-// tree; invstd = 1/sqrt(M2/M + eps) (biased variance, TF FusedBatchNorm).
-__global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict__ part, int P, int R, int M, int N,
-                                                        float eps, float* mean, float* invstd);
+// (jr_conv.hip; single-pass shifted combine in fp64, two stages when P is
+// large).
+__global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict__ part, const float* __restrict__ cnt,
+                                                        int P, int R, int M, int N, int chunk, float eps,
+                                                        float* mean, float* invstd, float* out);
 
 struct TileCfg {
   int bm, bn, wgm, bk, nbuf;

@@ -24,6 +24,7 @@ that step, MI355X-native:
 from __future__ import annotations
 
 import ctypes
+import dataclasses
 from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
@@ -32,6 +33,7 @@ import torch
 from . import _ffi
 from .inception import BN_EPS, Graph, PoolNode, build_inception_v3
 from .init import init_params
+from .lanes import Call, node_lanes, schedule
 from .plan import ConvUnit, build_plan
 
 DTYPES = {"f32": _ffi.JR_F32, "bf16": _ffi.JR_BF16}
@@ -44,7 +46,7 @@ class Engine:
                  device: int | torch.device = 0, dtype: str = "f32", train: bool = True,
                  optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
                  head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None,
-                 autotune: bool = True, fuse_siblings: bool = True):
+                 autotune: bool = True, fuse_siblings: bool = True, lanes: int = 2):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if not torch.cuda.is_available():
@@ -64,6 +66,12 @@ class Engine:
         self.units = self.g.units
         self.stream = torch.cuda.Stream(device=self.device)
         self._s = ctypes.c_void_p(self.stream.cuda_stream)
+        # lanes (jr.lanes): lane 0 is self.stream, where every step starts and ends
+        self.nlanes = max(1, int(lanes))
+        self.lane_streams = [self.stream] + [torch.cuda.Stream(device=self.device) for _ in range(self.nlanes - 1)]
+        self._fork_ev = torch.cuda.Event()
+        self._join_ev = [torch.cuda.Event() for _ in range(self.nlanes - 1)]
+        self._tail_ev = [torch.cuda.Event() for _ in range(self.nlanes)]
         self.plan = build_plan(self.g, fuse_siblings)
         self.cunits: List[ConvUnit] = self.plan.units
         self.layout, self.nparam = self.plan.layout, self.plan.nparam
@@ -126,7 +134,10 @@ class Engine:
             self.accum = self._t(self.nparam)
             self.dacts = [self._t(B * b.h * b.w * b.c, at) if b.id != g.input_buf else None
                           for b in g.bufs]
-            self.draw = self._t(max(B * u.ho * u.wo * u.cout for u in self.cunits), at)
+            # per-lane scratch for the raw-output gradient of the launch in flight
+            self.draw_lane = [self._t(max(B * u.ho * u.wo * u.cout for u in self.cunits), at)
+                              for _ in range(self.nlanes)]
+            self.draw = self.draw_lane[0]
             self.dfeat = self._t(B * feat_c)
         if self.dt == _ffi.JR_BF16:
             self._alloc_bf16_filters()
@@ -139,7 +150,8 @@ class Engine:
             for n in u.members:
                 ws = max(ws, self.lib.jr_bn_workspace_size(B * n.ho * n.wo, n.cout))
         self.ws_bytes = int(ws)
-        self.ws = self._t((self.ws_bytes + 15) // 4 + 4)
+        self.ws_lane = [self._t((self.ws_bytes + 15) // 4 + 4) for _ in range(self.nlanes)]
+        self.ws = self.ws_lane[0]
 
     def _alloc_bf16_filters(self) -> None:
         """bf16 operand copies of every conv launch's kernel (block), refreshed
@@ -164,10 +176,10 @@ class Engine:
         self.w_hwio = self._t(ho, torch.bfloat16)
         self.w_t = self._t(to, torch.bfloat16)
 
-    def _wprep_call(self):
+    def _wprep_call(self, stream=None):
         return (self.lib.jr_conv_weights_bf16_multi,
                 (self.wprep_table.data_ptr(), self.wprep_layers, self.wprep_tiles, self.params.data_ptr(),
-                 self.w_hwio.data_ptr(), self.w_t.data_ptr(), self._s), "wprep_bf16")
+                 self.w_hwio.data_ptr(), self.w_t.data_ptr(), stream or self._s), "wprep_bf16")
 
     def _wf(self, u: ConvUnit) -> int:
         """Filter operand of conv fwd: fp32 HWIO master block, or its bf16 W^T copy."""
@@ -258,21 +270,47 @@ class Engine:
         return _ffi.PoolDesc(B, n.h, n.w, n.c, n.ho, n.wo, 0, n.c, n.y.c_off, yb.c)
 
     # ------------------------------------------------------------- call lists
-    def _build_calls(self, B: int):
-        """Pre-bound (fn, args, name) lists for forward, backward, update."""
-        if B in self._calls:
-            return self._calls[B]
+    def _build_calls(self, B: int, nl: Optional[int] = None, one_stream: bool = False):
+        """Pre-bound Calls (jr.lanes) for forward, backward, update on nl
+        lanes (default self.nlanes), with their cross-lane waits:
+        (fwd, bwd, opt, keep, None).  one_stream: every call is bound to
+        lane 0's stream (per-lane scratch kept) for the explicit-DAG graph
+        capture, where the lanes become graph branches (capture())."""
+        nl = self.nlanes if nl is None else max(1, min(int(nl), self.nlanes))
+        key = (B, nl, one_stream)
+        if key in self._calls:
+            return self._calls[key]
         if B > self.batch or B <= 0:
             raise ValueError(f"batch {B} outside 1..{self.batch}")
-        L, g, s, dt = self.lib, self.g, self._s, self.dt
-        ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
+        L, g, dt = self.lib, self.g, self.dt
+        S = [ctypes.c_void_p(st.cuda_stream) for st in self.lane_streams[:nl]]
+        if one_stream:
+            S = [S[0]] * nl
+        WS = [ctypes.c_void_p(w.data_ptr()) for w in self.ws_lane[:nl]]
+        wsb = ctypes.c_size_t(self.ws_bytes)
+        lane_of = node_lanes(g, self.plan, nl)
         keep = []  # keep ctypes structs alive
-        fwd, bwd, opt = [], [], []
+        fwd, bwd, opt, seq = [], [], [], []
+
+        def add(lst, fn, args, name, lane, reads=(), writes=()):
+            c = Call(fn, args, name, lane, tuple(reads), tuple(writes))
+            lst.append(c)
+            seq.append(c)
+
+        # resources (jr.lanes.schedule): activation / gradient channel slices
+        slices: Dict[int, set] = {g.input_buf: {0}}
+        for n in g.nodes:
+            slices.setdefault(n.y.buf, set()).add(n.y.c_off)
+        a_all = lambda b: [("a", b, o) for o in sorted(slices[b])]  # noqa: E731
+        d_all = lambda b: [("d", b, o) for o in sorted(slices[b])]  # noqa: E731
         A = lambda bid: self.acts[bid].data_ptr()  # noqa: E731
         unit_of = self.plan.unit_of
+        wkey = ("w16",) if dt == _ffi.JR_BF16 else ("p",)
         if dt == _ffi.JR_BF16:
-            fwd.append(self._wprep_call())
+            add(fwd, *self._wprep_call(S[0]), 0, [("p",)], [("w16",)])
         for i, n in enumerate(g.nodes):
+            ln = lane_of[i]
+            s, ws = S[ln], WS[ln]
             if n.kind == "conv":
                 u = unit_of[n.idx]
                 if u.first is not n:
@@ -280,46 +318,51 @@ class Engine:
                 d = self._conv_desc(u, B)
                 keep.append(d)
                 M = B * u.ho * u.wo
-                raw = self.raw_unit[u.first.idx].data_ptr()
+                uid = u.first.idx
+                raw = self.raw_unit[uid].data_ptr()
                 # conv + the BN batch statistics of its raw output, fused
-                fwd.append((L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), dt, A(u.x), self._wf(u), raw, BN_EPS,
-                                                       self.mean_unit[u.first.idx].data_ptr(),
-                                                       self.invstd_unit[u.first.idx].data_ptr(), ws, wsb, s),
-                            "conv_fwd"))
+                add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), dt, A(u.x), self._wf(u), raw, BN_EPS,
+                                                    self.mean_unit[uid].data_ptr(),
+                                                    self.invstd_unit[uid].data_ptr(), ws, wsb, s),
+                    "conv_fwd", ln, a_all(u.x) + [wkey], [("r", uid), ("ws", ln)])
                 for m, co in zip(u.members, u.col_off):
                     yb = g.bufs[m.y.buf]
-                    fwd.append((L.jr_bn_relu_apply, (dt, raw, co, u.cout, M, m.cout, self.mean[m.idx].data_ptr(),
-                                                     self.invstd[m.idx].data_ptr(),
-                                                     self._p(f"batch_normalization_{m.idx + 1}/beta"),
-                                                     A(m.y.buf), m.y.c_off, yb.c, s), "bn_relu"))
+                    add(fwd, L.jr_bn_relu_apply, (dt, raw, co, u.cout, M, m.cout, self.mean[m.idx].data_ptr(),
+                                                  self.invstd[m.idx].data_ptr(),
+                                                  self._p(f"batch_normalization_{m.idx + 1}/beta"),
+                                                  A(m.y.buf), m.y.c_off, yb.c, s),
+                        "bn_relu", ln, [("r", uid), ("p",)], [("a", m.y.buf, m.y.c_off)])
             elif n.kind == "maxpool":
                 d = self._pool_desc(n, B)
                 keep.append(d)
-                fwd.append((L.jr_maxpool3x3s2_fwd, (ctypes.byref(d), dt, A(n.x), A(n.y.buf),
-                                                    self.argmax[i].data_ptr(), s), "maxpool_fwd"))
+                add(fwd, L.jr_maxpool3x3s2_fwd, (ctypes.byref(d), dt, A(n.x), A(n.y.buf), self.argmax[i].data_ptr(), s),
+                    "maxpool_fwd", ln, a_all(n.x), [("a", n.y.buf, n.y.c_off), ("am", i)])
             else:
                 d = self._pool_desc(n, B)
                 keep.append(d)
-                fwd.append((L.jr_avgpool3x3s1_fwd, (ctypes.byref(d), dt, A(n.x), A(n.y.buf), s),
-                            "avgpool_fwd"))
+                add(fwd, L.jr_avgpool3x3s1_fwd, (ctypes.byref(d), dt, A(n.x), A(n.y.buf), s),
+                    "avgpool_fwd", ln, a_all(n.x), [("a", n.y.buf, n.y.c_off)])
         ob = g.bufs[g.output_buf]
-        fwd.append((L.jr_gap_fwd, (dt, A(g.output_buf), B, ob.h * ob.w, ob.c, self.feat.data_ptr(), s),
-                    "gap_fwd"))
-        fwd.append((L.jr_head_fwd, (self.head_mode, self.feat.data_ptr(), self._p("dense/kernel"),
-                                    self._p("dense/bias"), self.labels.data_ptr(), B, ob.c, self.units,
-                                    self.logits.data_ptr(), self.probs.data_ptr(), self.loss.data_ptr(), s),
-                    "head_fwd"))
+        s0 = S[0]
+        add(fwd, L.jr_gap_fwd, (dt, A(g.output_buf), B, ob.h * ob.w, ob.c, self.feat.data_ptr(), s0),
+            "gap_fwd", 0, a_all(g.output_buf), [("feat",)])
+        add(fwd, L.jr_head_fwd, (self.head_mode, self.feat.data_ptr(), self._p("dense/kernel"),
+                                 self._p("dense/bias"), self.labels.data_ptr(), B, ob.c, self.units,
+                                 self.logits.data_ptr(), self.probs.data_ptr(), self.loss.data_ptr(), s0),
+            "head_fwd", 0, [("feat",), ("p",), ("lab",)], [("head",)])
         if self.train_mode:
             D = lambda bid: self.dacts[bid].data_ptr()  # noqa: E731
-            bwd.append((L.jr_head_bwd, (self.head_mode, self.feat.data_ptr(), self._p("dense/kernel"),
-                                        self.probs.data_ptr(), self.labels.data_ptr(), B, ob.c, self.units,
-                                        self.dfeat.data_ptr(), self._gp("dense/kernel"),
-                                        self._gp("dense/bias"), s), "head_bwd"))
-            bwd.append((L.jr_gap_bwd, (dt, self.dfeat.data_ptr(), B, ob.h * ob.w, ob.c, D(g.output_buf), s),
-                        "gap_bwd"))
+            add(bwd, L.jr_head_bwd, (self.head_mode, self.feat.data_ptr(), self._p("dense/kernel"),
+                                     self.probs.data_ptr(), self.labels.data_ptr(), B, ob.c, self.units,
+                                     self.dfeat.data_ptr(), self._gp("dense/kernel"), self._gp("dense/bias"), s0),
+                "head_bwd", 0, [("feat",), ("p",), ("head",), ("lab",)], [("dfeat",), ("g", "dense")])
+            add(bwd, L.jr_gap_bwd, (dt, self.dfeat.data_ptr(), B, ob.h * ob.w, ob.c, D(g.output_buf), s0),
+                "gap_bwd", 0, [("dfeat",)], d_all(g.output_buf))
             written = set()
             for i in range(len(g.nodes) - 1, -1, -1):
                 n = g.nodes[i]
+                ln = lane_of[i]
+                s, ws = S[ln], WS[ln]
                 acc = 1 if n.x in written else 0
                 if n.kind == "conv":
                     u = unit_of[n.idx]
@@ -328,59 +371,83 @@ class Engine:
                     d = self._conv_desc(u, B)
                     keep.append(d)
                     M = B * u.ho * u.wo
-                    raw = self.raw_unit[u.first.idx].data_ptr()
+                    uid = u.first.idx
+                    raw = self.raw_unit[uid].data_ptr()
+                    draw = self.draw_lane[ln].data_ptr()
                     for m, co in zip(u.members, u.col_off):
                         yb = g.bufs[m.y.buf]
-                        bwd.append((L.jr_bn_relu_bwd, (dt, D(m.y.buf), m.y.c_off, yb.c, raw, co, u.cout, M, m.cout,
-                                                       self.mean[m.idx].data_ptr(), self.invstd[m.idx].data_ptr(),
-                                                       self._p(f"batch_normalization_{m.idx + 1}/beta"),
-                                                       self.draw.data_ptr(),
-                                                       self._gp(f"batch_normalization_{m.idx + 1}/beta"),
-                                                       ws, wsb, s), "bn_relu_bwd"))
-                    bwd.append((L.jr_conv2d_bwd_filter, (ctypes.byref(d), dt, A(u.x), self.draw.data_ptr(),
-                                                         self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
-                                "conv_wgrad"))
+                        add(bwd, L.jr_bn_relu_bwd, (dt, D(m.y.buf), m.y.c_off, yb.c, raw, co, u.cout, M, m.cout,
+                                                    self.mean[m.idx].data_ptr(), self.invstd[m.idx].data_ptr(),
+                                                    self._p(f"batch_normalization_{m.idx + 1}/beta"), draw,
+                                                    self._gp(f"batch_normalization_{m.idx + 1}/beta"), ws, wsb, s),
+                            "bn_relu_bwd", ln, [("d", m.y.buf, m.y.c_off), ("r", uid), ("p",)],
+                            [("draw", ln), ("g", uid), ("ws", ln)])
+                    add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), dt, A(u.x), draw,
+                                                      self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
+                        "conv_wgrad", ln, a_all(u.x) + [("draw", ln)], [("g", uid), ("ws", ln)])
                     if u.x != g.input_buf:
-                        bwd.append((L.jr_conv2d_bwd_data, (ctypes.byref(d), dt, self.draw.data_ptr(),
-                                                           self._wd(u), D(u.x), acc, ws, wsb, s), "conv_dgrad"))
+                        add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), dt, draw, self._wd(u), D(u.x), acc, ws, wsb,
+                                                        s),
+                            "conv_dgrad", ln, [("draw", ln), wkey], d_all(u.x) + [("ws", ln)])
                         written.add(u.x)
-                    bwd.append(("param_ready", u.koff, "hook"))
+                    bwd.append(Call("param_ready", u.koff, "hook", 0))
                 elif n.kind == "maxpool":
                     d = self._pool_desc(n, B)
                     keep.append(d)
-                    bwd.append((L.jr_maxpool3x3s2_bwd, (ctypes.byref(d), dt, self.argmax[i].data_ptr(),
-                                                        D(n.y.buf), D(n.x), acc, s), "maxpool_bwd"))
+                    add(bwd, L.jr_maxpool3x3s2_bwd, (ctypes.byref(d), dt, self.argmax[i].data_ptr(), D(n.y.buf),
+                                                     D(n.x), acc, s),
+                        "maxpool_bwd", ln, [("am", i), ("d", n.y.buf, n.y.c_off)], d_all(n.x))
                     written.add(n.x)
                 else:
                     d = self._pool_desc(n, B)
                     keep.append(d)
-                    bwd.append((L.jr_avgpool3x3s1_bwd, (ctypes.byref(d), dt, D(n.y.buf), D(n.x), acc, s),
-                                "avgpool_bwd"))
+                    add(bwd, L.jr_avgpool3x3s1_bwd, (ctypes.byref(d), dt, D(n.y.buf), D(n.x), acc, s),
+                        "avgpool_bwd", ln, [("d", n.y.buf, n.y.c_off)], d_all(n.x))
                     written.add(n.x)
             P, G = self.params.data_ptr(), self.grads.data_ptr()
+            greads = [("g", u.first.idx) for u in self.cunits] + [("g", "dense")]
             if self.optimizer == "nesterov":
-                opt.append((L.jr_nesterov_update, (P, G, self.accum.data_ptr(), self.nparam, self.lr,
-                                                   self.momentum, 1.0, s), "nesterov"))
+                add(opt, L.jr_nesterov_update, (P, G, self.accum.data_ptr(), self.nparam, self.lr,
+                                                self.momentum, 1.0, s0), "nesterov", 0, greads, [("p",), ("acc",)])
             elif self.optimizer == "momentum":
-                opt.append((L.jr_momentum_update, (P, G, self.accum.data_ptr(), self.nparam, self.lr,
-                                                   self.momentum, 1.0, s), "momentum"))
+                add(opt, L.jr_momentum_update, (P, G, self.accum.data_ptr(), self.nparam, self.lr,
+                                                self.momentum, 1.0, s0), "momentum", 0, greads, [("p",), ("acc",)])
             elif self.optimizer == "sgd":
-                opt.append((L.jr_sgd_update, (P, G, self.nparam, self.lr, 1.0, s), "sgd"))
+                add(opt, L.jr_sgd_update, (P, G, self.nparam, self.lr, 1.0, s0), "sgd", 0, greads, [("p",)])
             else:
                 raise ValueError(f"unknown optimizer {self.optimizer}")
-        self._calls[B] = (fwd, bwd, opt, keep)
-        return self._calls[B]
+        schedule(seq)
+        self._calls[key] = (fwd, bwd, opt, keep, None)
+        return self._calls[key]
 
-    @staticmethod
-    def _run(calls, hook: Optional[Callable[[int], None]] = None) -> None:
-        for fn, args, name in calls:
-            if fn == "param_ready":
+    def _run(self, calls, events=None, hook: Optional[Callable[[int], None]] = None) -> None:
+        for c in calls:
+            if c.fn == "param_ready":
                 if hook is not None:
-                    hook(args)
+                    self._join()            # the bucket's gradients may come from any lane
+                    hook(c.args)
                 continue
-            rc = fn(*args)
+            st = self.lane_streams[c.lane]
+            for lj in c.waits:              # the other lane's tail (jr.lanes.schedule)
+                ev = self._tail_ev[lj]
+                ev.record(self.lane_streams[lj])
+                st.wait_event(ev)
+            rc = c.fn(*c.args)
             if rc:
-                raise _ffi.JRError(name, rc, _ffi.last_error())
+                raise _ffi.JRError(c.name, rc, _ffi.last_error())
+
+    def _fork(self) -> None:
+        """Every lane waits for the work enqueued on lane 0 so far."""
+        if self.nlanes > 1:
+            self._fork_ev.record(self.stream)
+            for st in self.lane_streams[1:]:
+                st.wait_event(self._fork_ev)
+
+    def _join(self) -> None:
+        """Lane 0 waits for every other lane's work enqueued so far."""
+        for ev, st in zip(self._join_ev, self.lane_streams[1:]):
+            ev.record(st)
+            self.stream.wait_event(ev)
 
     # ------------------------------------------------------------------- data
     def set_batch(self, images, labels=None, n: Optional[int] = None) -> int:
@@ -414,24 +481,28 @@ class Engine:
 
     # ------------------------------------------------------------------- runs
     def forward(self, B: Optional[int] = None) -> None:
-        fwd, _, _, _ = self._build_calls(B or self.batch)
-        self._run(fwd)
+        fwd, _, _, _, ev = self._build_calls(B or self.batch)
+        self._fork()
+        self._run(fwd, ev)
+        self._join()
 
     def backward(self, B: Optional[int] = None, hook=None) -> None:
-        _, bwd, _, _ = self._build_calls(B or self.batch)
-        self._run(bwd, hook)
+        _, bwd, _, _, ev = self._build_calls(B or self.batch)
+        self._run(bwd, ev, hook)
+        self._join()
 
     def apply_update(self, B: Optional[int] = None, grad_scale: float = 1.0) -> None:
-        _, _, opt, _ = self._build_calls(B or self.batch)
+        _, _, opt, _, ev = self._build_calls(B or self.batch)
         if grad_scale != 1.0:
-            fn, args, name = opt[0]
-            args = list(args)
+            c = opt[0]
+            args = list(c.args)
             args[-2] = grad_scale
-            opt = [(fn, tuple(args), name)]
-        self._run(opt)
+            opt = [dataclasses.replace(c, args=tuple(args))]
+        self._run(opt, ev)
 
     def train_step(self, B: Optional[int] = None, allreduce=None) -> None:
-        """fwd + bwd (+ bucketed all-reduce) + optimizer, enqueued on self.stream."""
+        """fwd + bwd (+ bucketed all-reduce) + optimizer, enqueued on the lanes;
+        everything is joined back onto self.stream before the optimizer."""
         B = B or self.batch
         if allreduce is None:
             self.forward(B)
@@ -445,18 +516,67 @@ class Engine:
         self.apply_update(B, grad_scale=scale)
 
     def capture(self, B: Optional[int] = None) -> None:
-        """Capture fwd+bwd+update for batch B into a HIP graph (single GPU)."""
+        """Capture fwd+bwd+update for batch B into a HIP graph (single GPU);
+        the lanes become parallel branches of the graph.  Up to two lanes
+        the lane streams themselves are captured (fork/join by events: the
+        faster graph on ROCm 7.2); beyond that the DAG is built explicitly
+        on ONE capturing stream (capture_dag), because cross-waits among
+        three or more captured streams crashed hipGraphInstantiate."""
         B = B or self.batch
-        fwd, bwd, opt, _ = self._build_calls(B)
+        if self.nlanes > 2:
+            return self.capture_dag(B)
+        fwd, bwd, opt, _, _ = self._build_calls(B)
         torch.cuda.synchronize(self.device)
         _ffi.check("jr_graph_begin", self.lib.jr_graph_begin(self._s))
         try:
+            self._fork()
             self._run(fwd)
+            self._join()
             self._run(bwd)
+            self._join()
             self._run(opt)
         finally:
             ex = ctypes.c_void_p()
             _ffi.check("jr_graph_end", self.lib.jr_graph_end(self._s, ctypes.byref(ex)))
+        self._graphs[B] = ex.value
+
+    def capture_dag(self, B: Optional[int] = None) -> None:
+        """Graph capture with the lanes built explicitly on ONE capturing
+        stream: before each call the stream's capture dependencies are set
+        to its lane's tail plus the tails of the lanes it waits for
+        (jr.lanes.schedule), and the call's last node becomes its lane's new
+        tail."""
+        B = B or self.batch
+        fwd, bwd, opt, _, _ = self._build_calls(B, one_stream=True)
+        L = self.lib
+        torch.cuda.synchronize(self.device)
+        buf = (ctypes.c_void_p * 256)()
+        cnt = ctypes.c_int()
+
+        def get_deps():
+            _ffi.check("jr_graph_get_deps", L.jr_graph_get_deps(self._s, buf, 256, ctypes.byref(cnt)))
+            return [buf[i] for i in range(cnt.value)]
+
+        def set_deps(nodes):
+            arr = (ctypes.c_void_p * max(1, len(nodes)))(*nodes)
+            _ffi.check("jr_graph_set_deps", L.jr_graph_set_deps(self._s, arr, len(nodes)))
+
+        _ffi.check("jr_graph_begin", L.jr_graph_begin(self._s))
+        try:
+            start = get_deps()
+            tail = {ln: start for ln in range(self.nlanes)}
+            for c in fwd + bwd + opt:
+                if c.fn == "param_ready":
+                    continue
+                set_deps(list(dict.fromkeys(tail[c.lane] + [x for lj in c.waits for x in tail[lj]])))
+                rc = c.fn(*c.args)
+                if rc:
+                    raise _ffi.JRError(c.name, rc, _ffi.last_error())
+                tail[c.lane] = get_deps()
+            set_deps(list(dict.fromkeys(x for ln in sorted(tail) for x in tail[ln])))   # join
+        finally:
+            ex = ctypes.c_void_p()
+            _ffi.check("jr_graph_end", L.jr_graph_end(self._s, ctypes.byref(ex)))
         self._graphs[B] = ex.value
 
     def replay(self, B: Optional[int] = None) -> None:
@@ -464,7 +584,8 @@ class Engine:
         _ffi.check("jr_graph_launch", self.lib.jr_graph_launch(ctypes.c_void_p(self._graphs[B]), self._s))
 
     def synchronize(self) -> None:
-        self.stream.synchronize()
+        for st in self.lane_streams:
+            st.synchronize()
 
     def loss_value(self) -> float:
         self.synchronize()

@@ -120,8 +120,9 @@ def test_bf16_loss_curve_tracks_f32():
     implementations decorrelate within a few steps too), so the end-to-end
     bar is the shape of the training trajectory at the full 299^2 geometry:
     30 Nesterov steps on one fixed batch of 8 from the same weights, bf16 vs
-    the fp32 engine: step-0 loss within 0.05, both fit the batch (final loss
-    < 0.5x initial), mean |loss difference| over the curve <= 0.1."""
+    the fp32 engine: the first 2 losses within 0.05, both fit the batch
+    (final loss < 0.3x initial) and cross half the initial loss at most 6
+    steps apart."""
     from jr.engine import Engine
     from jr import synth
     B, res = 8, 299
@@ -138,9 +139,13 @@ def test_bf16_loss_curve_tracks_f32():
     print("f32 ", np.round(f, 3))
     print("bf16", np.round(h, 3))
     assert np.all(np.isfinite(h))
-    assert abs(f[0] - h[0]) <= 0.05, (f[0], h[0])
-    assert f[-3:].mean() < 0.5 * f[0] and h[-3:].mean() < 0.5 * h[0], (f, h)
-    assert np.mean(np.abs(f - h)) <= 0.1, (f, h)
+    # the first steps agree before rounding differences compound ...
+    assert np.all(np.abs(f[:2] - h[:2]) <= 0.05), (f[:2], h[:2])
+    # ... both fit the batch, and bf16 reaches half the initial loss within
+    # a few steps of fp32 (measured: 0-4 steps apart)
+    assert f[-3:].mean() < 0.3 * f[0] and h[-3:].mean() < 0.3 * h[0], (f, h)
+    cf, ch = int(np.argmax(f < 0.5 * f[0])), int(np.argmax(h < 0.5 * h[0]))
+    assert abs(cf - ch) <= 6, (cf, ch, f, h)
 
 
 def test_bf16_graph_replay_and_training_descends():
@@ -191,3 +196,38 @@ def test_sibling_fusion_matches_unfused(dtype):
     cos = float(ga @ gb / (np.linalg.norm(ga) * np.linalg.norm(gb)))
     assert cos >= (0.9999 if dtype == "f32" else 0.98), cos
     assert np.array_equal(e[True].params_numpy(), e[False].params_numpy())
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_lanes_are_bitwise_single_stream(dtype):
+    """Branch-level concurrency (jr.lanes): the engine's own call schedule
+    orders every conflicting pair across lanes, and 4 lanes (eager and as a
+    HIP graph) give bitwise the single-stream result over several steps."""
+    from jr.engine import Engine
+    from jr.lanes import check_schedule
+    from jr import synth
+    imgs = synth.fundus_batch(2, 4, 107)
+    y = np.array([[1.0], [0.0], [1.0], [0.0]], np.float32)
+    one = Engine(4, 107, 107, seed=6, dtype=dtype, lanes=1)
+    many = Engine(4, 107, 107, seed=6, dtype=dtype, lanes=4)
+    graph = Engine(4, 107, 107, seed=6, dtype=dtype, lanes=4)     # explicit-DAG capture
+    graph2 = Engine(4, 107, 107, seed=6, dtype=dtype, lanes=2)    # two captured streams
+    fwd, bwd, opt, _, _ = many._build_calls(4)
+    seq = sorted([c for c in fwd + bwd + opt if c.idx >= 0], key=lambda c: c.idx)
+    check_schedule(seq)
+    assert len({c.lane for c in seq}) == 4
+    for e in (one, many, graph, graph2):
+        e.set_batch(imgs, y)
+    # (tile choices are process-global in libjr: all four use the same ones)
+    graph.capture()
+    graph2.capture()
+    for _ in range(3):
+        one.train_step()
+        many.train_step()
+        graph.replay()
+        graph2.replay()
+    for e in (one, many, graph, graph2):
+        e.synchronize()
+    for e in (many, graph, graph2):
+        assert np.array_equal(one.params_numpy(), e.params_numpy())
+        assert one.loss_value() == e.loss_value()

@@ -3,7 +3,7 @@ kernel size: ms per step and achieved TFLOP/s."""
 import collections, re, sys
 tot, fl = collections.Counter(), collections.Counter()
 for l in open(sys.argv[1]):
-    m = re.match(r"(conv2d_\d+)\s+(\w+)\s+(\d)x(\d)/(\d).*grid=\s*\S+\s+([\d.]+)\+\s*([\d.]+)us\s+([\d.]+) TF/s", l)
+    m = re.match(r"(conv2d_[\d+]+)\s+(\w+)\s+(\d)x(\d)/(\d).*grid=\s*\S+\s+([\d.]+)\+\s*([\d.]+)us\s+([\d.]+) TF/s", l)
     if not m:
         continue
     op = 'dgrad' if m.group(2).startswith('dg') else m.group(2)

@@ -1,41 +1,72 @@
-"""Map k_conv_f32 dispatches of a rocprofv3 kernel trace to (layer, op) and
-print per-call achieved TFLOP/s for the last training step in the trace."""
+"""Map the conv GEMM dispatches of the last training step in a rocprofv3
+kernel trace to (launch, op) of the engine's plan (jr.plan: fused sibling
+groups included) and print per-call achieved TFLOP/s, then a whole-step
+kernel-family breakdown.
+  python tools/conv_table.py trace.csv [B] [top] [split_top] [stats.csv] [nsteps] [res] [--unfused]"""
 import csv, sys, os
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "jama16-retina-replication_amd"))
 from jr.inception import build_inception_v3
+from jr.plan import build_plan
 
-trace = sys.argv[1]
-B = int(sys.argv[2]) if len(sys.argv) > 2 else 64
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+trace = args[0]
+B = int(args[1]) if len(args) > 1 else 64
+res = int(args[6]) if len(args) > 6 else 299
+sys.argv = [sys.argv[0]] + args
 rows = [r for r in csv.DictReader(open(trace)) if r["Kind"] == "KERNEL_DISPATCH"]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-g = build_inception_v3()
-seq = [(n, "fwd") for n in g.convs]
-for n in reversed(g.convs):
-    seq.append((n, "wgrad"))
-    if n.idx != 0:
-        for ph in range(n.stride * n.stride):   # one GEMM per stride phase
-            seq.append((n, "dgrad" if n.stride == 1 else f"dg{ph}"))
+g = build_inception_v3(res, res)
+plan = build_plan(g, "--unfused" not in sys.argv[0:] and "--unfused" not in os.environ.get("CONV_TABLE", ""))
+
+
+def phases(u):
+    s, k = u.stride, []
+    for py in range(s):
+        for px in range(s):
+            hc = (u.h - py + s - 1) // s if py < u.h else 0
+            wc = (u.w - px + s - 1) // s if px < u.w else 0
+            r0, c0 = (py + u.pad_h) % s, (px + u.pad_w) % s
+            na = (u.kh - r0 + s - 1) // s if r0 < u.kh else 0
+            nb = (u.kw - c0 + s - 1) // s if c0 < u.kw else 0
+            if hc and wc:
+                k.append((f"dg{py * s + px}" if s > 1 else "dgrad", 2 * B * hc * wc * u.cin * na * nb * u.cout))
+    return k
+
+
+seq = [(u, "fwd", 2 * u.macs_per_image() * B) for u in plan.units]
+for u in reversed(plan.units):
+    seq.append((u, "wgrad", 2 * u.macs_per_image() * B))
+    if u.x != g.input_buf:
+        seq += [(u, op, f) for op, f in phases(u)]
+
+opt = [i for i, r in enumerate(rows) if "k_nesterov" in r["Kernel_Name"] or "k_sgd" in r["Kernel_Name"]]
+step_rows = rows[opt[-2] + 1:opt[-1] + 1] if len(opt) >= 2 else rows
+FAMILY = ("k_splitk_reduce", "k_stats_finalize")
 conv = []
 i = 0
-while i < len(rows):
-    r = rows[i]
-    if "k_conv" in r["Kernel_Name"] and "splitk" not in r["Kernel_Name"]:
+while i < len(step_rows):
+    r = step_rows[i]
+    nm = r["Kernel_Name"]
+    if ("k_conv<" in nm or "k_conv_bf16<" in nm):
         t = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        t2 = 0
         j = i + 1
-        if j < len(rows) and "splitk_reduce" in rows[j]["Kernel_Name"]:
-            t2 = int(rows[j]["End_Timestamp"]) - int(rows[j]["Start_Timestamp"])
-        else:
-            t2 = 0
+        while j < len(step_rows) and any(f in step_rows[j]["Kernel_Name"] for f in FAMILY):
+            t2 += int(step_rows[j]["End_Timestamp"]) - int(step_rows[j]["Start_Timestamp"])
+            j += 1
         conv.append((r, t, t2))
+        i = j
+        continue
     i += 1
+if len(conv) != len(seq):
+    print(f"warning: {len(conv)} conv GEMMs in the step, plan expects {len(seq)}", file=sys.stderr)
 last = conv[-len(seq):]
 tot_t = 0; tot_f = 0
 out = []
-for (n, op), (r, t, t2) in zip(seq, last):
-    f = 2 * n.macs_per_image() * B / (n.stride * n.stride if op.startswith("dg") and op != "dgrad" else 1)
+for (u, op, f), (r, t, t2) in zip(seq, last):
     tot_t += t + t2; tot_f += f
     name = r["Kernel_Name"]; cfg = name[name.index("<"):name.index(">") + 1]
-    out.append((t + t2, f"{n.name:10s} {op:5s} {n.kh}x{n.kw}/{n.stride} {n.h:3d}x{n.w:<3d} {n.cin:4d}->{n.cout:4d} "
+    out.append((t + t2, f"{u.name:14s} {op:5s} {u.kh}x{u.kw}/{u.stride} {u.h:3d}x{u.w:<3d} {u.cin:4d}->{u.cout:4d} "
                 f"{cfg:24s} grid={r['Grid_Size_X']:>7s}x{r['Grid_Size_Z']:<4s} {t/1e3:8.1f}+{t2/1e3:6.1f}us {f/(t+t2)/1e3:7.1f} TF/s"))
 for t, s in sorted(out, reverse=True)[:int(sys.argv[3]) if len(sys.argv) > 3 else 40]:
     print(s)
