@@ -41,7 +41,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=None, help="per GPU (default 64 train, 32 eval)")
+    ap.add_argument("--mode", default="train", choices=["train", "eval"],
+                    help="eval: forward only with batch-statistics BN, the ensemble member pass of "
+                         "evaluate.py:166-211 (BASELINE config 4)")
     ap.add_argument("--res", type=int, default=299)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a HIP graph")
@@ -62,7 +65,7 @@ def conv_roofline(eng, steps: int = 3):
     flops = 0
     for n in eng.g.convs:
         m = n.macs_per_image() * eng.batch
-        flops += 2 * m * (2 if n.x == eng.g.input_buf else 3)
+        flops += 2 * m * ((2 if n.x == eng.g.input_buf else 3) if eng.train_mode else 1)
     pairs = []
     for _ in range(steps):
         for calls in (fwd, bwd, opt):
@@ -146,24 +149,27 @@ def main():
     from jr import synth
     from jr.dist import BucketAllReduce
 
-    B, res = args.batch, args.res
-    eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0, lanes=args.lanes)
+    train = args.mode == "train"
+    B, res = args.batch or (64 if train else 32), args.res
+    eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0, lanes=args.lanes, train=train)
     imgs = synth.fundus_batch(rank * B, B, res)
     labels = synth.labels(rank * B, B)
     eng.set_batch(imgs, labels)
     eng.synchronize()
-    ar = BucketAllReduce(eng, world) if world > 1 else None
+    ar = BucketAllReduce(eng, world) if world > 1 and train else None
     use_graph = (not args.no_graph) and ar is None
 
     def step():
         if use_graph:
             eng.replay()
-        else:
+        elif train:
             eng.train_step(allreduce=ar)
+        else:
+            eng.forward()
 
     for i in range(args.warmup):
         if use_graph and i == 0:
-            eng.train_step()           # first step eager (plans, workspaces)
+            eng.train_step() if train else eng.forward()   # first step eager (plans, workspaces)
             eng.synchronize()
             eng.capture()
             continue
@@ -186,9 +192,9 @@ def main():
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    loss = eng.loss_value()
+    loss = eng.loss_value() if train else float(np.mean(eng.predictions()))
     if not np.isfinite(loss):
-        raise SystemExit(f"non-finite loss {loss}")
+        raise SystemExit(f"non-finite {'loss' if train else 'prediction'} {loss}")
 
     out = None
     if rank == 0:
@@ -201,23 +207,27 @@ def main():
             peak = PEAK_TFLOPS[args.dtype]
             roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": None,
-                    "kernel": f"conv implicit-GEMM fwd+dgrad+wgrad ({nconv} calls/step)",
+                    "kernel": f"conv implicit-GEMM {'fwd+dgrad+wgrad' if train else 'fwd'} ({nconv} calls/step)",
                     "conv_ms_per_step": round(tconv * 1e3, 3),
                     "algorithmic_gflop_per_step": round(flops / 1e9, 1)}
-            roof.update(pmc_traffic(args.dtype, B, res))
+            if train:
+                roof.update(pmc_traffic(args.dtype, B, res))
         out = {
-            "metric": "train images/sec, Inception-v3 299^2 bs64/GPU",
+            "metric": (f"train images/sec, Inception-v3 {res}^2 bs{B}/GPU" if train else
+                       f"eval images/sec, Inception-v3 {res}^2 bs{B}/GPU (one ensemble member, batch-stat BN)"),
             "value": round(imgs_s, 2), "unit": "images/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": args.dtype, "data": "synthetic fundus-shaped uint8 299x299x3 (jr.synth), random Keras init",
-            "config": {"workload": f"Inception-v3 {res}x{res} {args.dtype} training, batch {B}/GPU, "
-                                   f"Nesterov lr 3e-3 m 0.9", "model": "inception_v3", "global_batch": B * world,
+            "dtype": args.dtype, "data": f"synthetic fundus-shaped uint8 {res}x{res}x3 (jr.synth), random Keras init",
+            "config": {"workload": (f"Inception-v3 {res}x{res} {args.dtype} training, batch {B}/GPU, "
+                                    f"Nesterov lr 3e-3 m 0.9" if train else
+                                    f"Inception-v3 {res}x{res} {args.dtype} forward (evaluate.py), batch {B}/GPU, "
+                                    f"batches sharded over ranks"), "model": "inception_v3", "global_batch": B * world,
                        "seq_len": None, "parallelism": f"dp{world}", "hip_graph": use_graph, "lanes": args.lanes},
-            "final_loss": round(loss, 5),
+            ("final_loss" if train else "mean_prediction"): round(loss, 5),
             "roofline": roof,
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and train:
             out["cpu_baseline"] = cpu_baseline(args, res)
         print(json.dumps(out), flush=True)
     if dist:
