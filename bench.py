@@ -32,7 +32,11 @@ sys.path.insert(0, os.path.join(ROOT, "jama16-retina-replication_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA (MI355X_MICROARCH.md)
+# MI355X dense MFMA (MI355X_MICROARCH.md); x8 = eight bf16 MFMAs per fp32 product
+PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0, "x8": round(2500.0 / 8, 1)}
+CONV_MATH = {"f32": "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
+             "x8": "fp32 via exact 3-way bf16 split, 8 bf16 MFMAs per product (all terms > 2^-32), "
+                   "fp32 accumulate (JR_F32_X8)"}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -47,6 +51,9 @@ def parse():
                          "evaluate.py:166-211 (BASELINE config 4)")
     ap.add_argument("--res", type=int, default=299)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--conv-math", default="x8", choices=["f32", "x8"],
+                    help="dtype f32 only. x8 (default): fp32 tensors, products from an exact 3-way bf16 split "
+                         "(jr.h JR_F32_X8, fp32-accurate); f32: fp32 MFMA")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a HIP graph")
     ap.add_argument("--lanes", type=int, default=2, help="streams for branch-level concurrency (jr.lanes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -151,7 +158,9 @@ def main():
 
     train = args.mode == "train"
     B, res = args.batch or (64 if train else 32), args.res
-    eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0, lanes=args.lanes, train=train)
+    math = args.conv_math if args.dtype == "f32" else "bf16"
+    eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0, lanes=args.lanes, train=train,
+                 conv_math=math)
     imgs = synth.fundus_batch(rank * B, B, res)
     labels = synth.labels(rank * B, B)
     eng.set_batch(imgs, labels)
@@ -204,7 +213,7 @@ def main():
         if not args.no_roofline:
             flops, tconv, nconv = conv_roofline(eng)
             ach = flops / tconv / 1e12
-            peak = PEAK_TFLOPS[args.dtype]
+            peak = PEAK_TFLOPS["x8" if math == "x8" else args.dtype]
             roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": None,
                     "kernel": f"conv implicit-GEMM {'fwd+dgrad+wgrad' if train else 'fwd'} ({nconv} calls/step)",
@@ -223,7 +232,8 @@ def main():
                                     f"Nesterov lr 3e-3 m 0.9" if train else
                                     f"Inception-v3 {res}x{res} {args.dtype} forward (evaluate.py), batch {B}/GPU, "
                                     f"batches sharded over ranks"), "model": "inception_v3", "global_batch": B * world,
-                       "seq_len": None, "parallelism": f"dp{world}", "hip_graph": use_graph, "lanes": args.lanes},
+                       "seq_len": None, "parallelism": f"dp{world}", "hip_graph": use_graph, "lanes": args.lanes,
+                       "conv_math": CONV_MATH[args.conv_math] if args.dtype == "f32" else "bf16 MFMA"},
             ("final_loss" if train else "mean_prediction"): round(loss, 5),
             "roofline": roof,
         }

@@ -23,7 +23,15 @@
  *    given stream (hipStream_t passed as void*; NULL = the null stream), so a
  *    whole training step can be captured into a HIP graph.
  *  - dtype: JR_F32 = IEEE fp32 end to end (the reference's precision);
- *    JR_BF16 = bf16 activations/weights with fp32 accumulation.
+ *    JR_BF16 = bf16 activations/weights with fp32 accumulation;
+ *    JR_F32_X8 (convolution entry points only) = fp32 tensors exactly as
+ *    JR_F32, the GEMM products formed on the bf16 matrix cores: every fp32
+ *    operand is split exactly into three bf16 terms (x = h + m + l) and eight
+ *    bf16 MFMAs accumulate hh+hm+mh+mm+hl+lh+ml+lm in fp32; only l*l
+ *    (< 2^-32 |a b|) is dropped, so every product is exact to far below
+ *    fp32 rounding and the result differs from JR_F32 only in summation
+ *    order (bf16x9-style fp32 emulation).  Non-finite inputs give NaN where
+ *    JR_F32 could give +-inf.
  */
 #ifndef JR_H_
 #define JR_H_
@@ -43,7 +51,7 @@ typedef enum jr_status {
   JR_ERR_WORKSPACE = -4    /* workspace smaller than *_workspace_size      */
 } jr_status;
 
-typedef enum jr_dtype { JR_F32 = 0, JR_BF16 = 1 } jr_dtype;
+typedef enum jr_dtype { JR_F32 = 0, JR_BF16 = 1, JR_F32_X8 = 2 } jr_dtype;
 
 typedef enum jr_conv_op { JR_CONV_FWD = 0, JR_CONV_BWD_DATA = 1, JR_CONV_BWD_FILTER = 2 } jr_conv_op;
 
@@ -117,7 +125,8 @@ int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const void* a, 
                        void* ws, size_t ws_bytes, void* stream);
 /* Tile configuration the next call would use (DGRAD: per stride phase),
  * and an explicit override (reproducibility, tests).  A config id is
- * tile | (splits << 8), splits = 0: planner's split-K factor. */
+ * tile | (splits << 8), splits = 0: planner's split-K factor; set_config
+ * with cfg = -1 drops the override (autotuned or set) for that GEMM. */
 int jr_conv2d_get_config(const jr_conv_desc* d, int op, int dtype, int phase);
 int jr_conv2d_set_config(const jr_conv_desc* d, int op, int dtype, int phase, int cfg);
 int jr_conv2d_num_configs(int dtype);   /* tiles of that dtype's table */

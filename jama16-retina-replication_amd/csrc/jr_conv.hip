@@ -42,6 +42,71 @@
 
 namespace jr {
 
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {   // v_cvt_pk_bf16_f32 (RNE), a in the low half
+  const bf16x2 r = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, r);
+}
+
+// a - b as a plain v_sub_f32: hipcc otherwise SLP-packs the pairs into
+// v_pk_add_f32, which costs more than two scalar ops beside MFMAs
+// (MI355X_MICROARCH.md cycle constants)
+__device__ __forceinline__ float sub_f32(float a, float b) {
+  float r;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Exact three-way split of 8 fp32 values into bf16 (SplitFrag): x = h + m + l with
+// h = rne(x), m = rne(x - h), l = x - h - m (the remainders are exact in
+// fp32; x - h has at most 16 significant bits, x - h - m at most 8, so l is
+// exact in bf16).  |m| <= 2^-8 |x|, |l| <= 2^-16 |x| (normal range).  Done
+// in three stages, so each stage's VALU can hide under the MFMAs of the
+// terms the previous stage made available: init = h (one cvt per pair),
+// stage2 = r = x - h and m, stage3 = r - m and l.  skip = diagnostic (no
+// split: the fp32 bits reinterpreted).
+// bf16 products per fp32 product: 8 = hh hm mh mm hl lh ml lm, dropping only
+// ll (< 2^-32 |a b|).  6 (also dropping ml + lm, up to 2^-23 |a b|: the size
+// of fp32's own rounding) measured 8 % faster per step but ~1.5-2x the
+// fp32 kernel's error on long reductions; 8 matches it.
+constexpr int kSplitTerms = 8;
+
+struct SplitFrag {
+  float x[8];
+  uint32_t hp[4], mp[4], lp[4];
+  __device__ __forceinline__ void init(const float* v, bool skip) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) x[t] = v[t];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) hp[p] = skip ? __float_as_uint(x[2 * p]) : pk_bf16(x[2 * p], x[2 * p + 1]);
+  }
+  __device__ __forceinline__ void stage2(bool skip) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (skip) { mp[p] = hp[p]; continue; }
+      x[2 * p] = sub_f32(x[2 * p], __uint_as_float(hp[p] << 16));
+      x[2 * p + 1] = sub_f32(x[2 * p + 1], __uint_as_float(hp[p] & 0xffff0000u));
+      mp[p] = pk_bf16(x[2 * p], x[2 * p + 1]);
+    }
+  }
+  __device__ __forceinline__ void stage3(bool skip) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (skip) { lp[p] = hp[p]; continue; }
+      x[2 * p] = sub_f32(x[2 * p], __uint_as_float(mp[p] << 16));
+      x[2 * p + 1] = sub_f32(x[2 * p + 1], __uint_as_float(mp[p] & 0xffff0000u));
+      lp[p] = pk_bf16(x[2 * p], x[2 * p + 1]);
+    }
+  }
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  __device__ __forceinline__ bf16x8 h() const { return __builtin_bit_cast(bf16x8, (u32x4){hp[0], hp[1], hp[2], hp[3]}); }
+  __device__ __forceinline__ bf16x8 m() const { return __builtin_bit_cast(bf16x8, (u32x4){mp[0], mp[1], mp[2], mp[3]}); }
+  __device__ __forceinline__ bf16x8 l() const { return __builtin_bit_cast(bf16x8, (u32x4){lp[0], lp[1], lp[2], lp[3]}); }
+};
+
 // DBG (diagnostic builds only, jr_conv2d_debug_time): 1 = no MFMA,
 // 2 = no DMA after the first tile (results are wrong in both).
 //
@@ -53,7 +118,7 @@ namespace jr {
 // (conv1, c_in = 3 padded to 4) every lane keeps its own mixed-radix k
 // counter (generic path).  WGRAD's A operand walks pixels along k, so its
 // lanes advance (b, oh, ow) counters.
-template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, int DBG = 0>
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0>
 __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int WGN = 4 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -369,6 +434,85 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
         }
       }
     }
+    if constexpr (X8) {
+      // JR_F32_X8: each lane's 8 consecutive k of a lane half are exactly the
+      // A / B operand of one v_mfma_f32_32x32x16_bf16 (lane l: row l % 32,
+      // k = 8 (l / 32) + 0..7 of the group), so the fp32 fragments split in
+      // registers into x = h + m + l (three bf16, exact) and kSplitTerms bf16
+      // MFMAs accumulate the partial products in fp32 (SplitFrag).
+      constexpr int G8 = HALF / 8;
+      static_assert(HALF % 8 == 0, "X8 needs BK % 16 == 0");
+      // Three MFMA phases per 16-k group, each a scheduling region closed by
+      // a DMA piece (the LDS-DMA intrinsic is a scheduling boundary), each
+      // carrying the VALU the NEXT phase needs so the split hides under MFMAs:
+      //   P1: h packs (cheap: one cvt per pair) | hh MFMAs + residuals, m packs
+      //   P2: hm mh mm MFMAs + second residuals, l packs
+      //   P3: hl lh (ml lm) MFMAs
+      // Terms are added largest first.
+      int piece = 0;
+      auto next_piece = [&]() {
+        if constexpr (DO_ISSUE && DBG != 2) {
+          if (piece < NPIECE) issue_piece(kt + NBUF - 1, piece, wA, wB);
+          ++piece;
+        }
+      };
+      auto mma = [&](int i, int j, const bf16x8& x, const bf16x8& y) {
+        if constexpr (DBG == 1) {   // diagnostic: no MFMA (keeps the operands live)
+          const f32x4 t = __builtin_bit_cast(f32x4, x) + __builtin_bit_cast(f32x4, y);
+          acc[i][j][0] += t[0]; acc[i][j][1] += t[1]; acc[i][j][2] += t[2]; acc[i][j][3] += t[3];
+        } else {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc[i][j], 0, 0, 0);
+        }
+      };
+#pragma unroll
+      for (int g8 = 0; g8 < G8; ++g8) {
+        SplitFrag sa[TM], sb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) sa[i].init(&af[i][8 * g8], DBG == 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) sb[j].init(&bfr[j][8 * g8], DBG == 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) mma(i, j, sa[i].h(), sb[j].h());
+#pragma unroll
+        for (int i = 0; i < TM; ++i) sa[i].stage2(DBG == 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) sb[j].stage2(DBG == 4);
+        next_piece();
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            mma(i, j, sa[i].h(), sb[j].m());
+            mma(i, j, sa[i].m(), sb[j].h());
+            mma(i, j, sa[i].m(), sb[j].m());
+          }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) sa[i].stage3(DBG == 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) sb[j].stage3(DBG == 4);
+        next_piece();
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            mma(i, j, sa[i].h(), sb[j].l());
+            mma(i, j, sa[i].l(), sb[j].h());
+            if constexpr (kSplitTerms == 8) {
+              mma(i, j, sa[i].m(), sb[j].l());
+              mma(i, j, sa[i].l(), sb[j].m());
+            }
+          }
+        next_piece();
+      }
+      if constexpr (DO_ISSUE && DBG != 2) {
+#pragma unroll
+        for (int d = 3 * G8; d < NPIECE; ++d) issue_piece(kt + NBUF - 1, d, wA, wB);
+        advance();
+      }
+      return;
+    }
     // MFMAs of k-step s, then DMA piece s of tile kt+NBUF-1: program order
     // places each piece's address VALU and issue under an MFMA group in
     // flight (the LDS-DMA intrinsic is a scheduling boundary for hipcc).
@@ -572,40 +716,40 @@ static size_t stats_ws(int dtype, const Plan& p) {
 
 // Fast-path kernels (UT): FWD/DGRAD when the reduction channel radix is a
 // multiple of BK (every layer but conv1 FWD at BK = 16); WGRAD when wo >= BK.
-template <int OP, int C, int DBG>
+template <int OP, int C, int DBG, bool X8>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t s) {
   constexpr TileCfg t = kCfgs[C];
   const bool fast = OP == OP_WGRAD ? a.wo >= t.bk : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
   if (fast) {
-    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, DBG>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, X8, DBG>), grid, dim3(256), 0, s, a);
     return;
   }
   if constexpr (DBG == 0)
-    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, 0>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, X8, 0>), grid, dim3(256), 0, s, a);
 }
 
-template <int OP, int DBG = 0>
+template <int OP, int DBG = 0, bool X8 = false>
 static void launch_op(int cfg, const ConvArgs& a, dim3 grid, hipStream_t s) {
   switch (cfg) {
-    case 0: launch_cfg<OP, 0, DBG>(a, grid, s); break;
-    case 1: launch_cfg<OP, 1, DBG>(a, grid, s); break;
-    case 2: launch_cfg<OP, 2, DBG>(a, grid, s); break;
-    case 3: launch_cfg<OP, 3, DBG>(a, grid, s); break;
-    case 4: launch_cfg<OP, 4, DBG>(a, grid, s); break;
-    case 5: launch_cfg<OP, 5, DBG>(a, grid, s); break;
-    case 6: launch_cfg<OP, 6, DBG>(a, grid, s); break;
-    case 7: launch_cfg<OP, 7, DBG>(a, grid, s); break;
-    case 8: launch_cfg<OP, 8, DBG>(a, grid, s); break;
-    case 9: launch_cfg<OP, 9, DBG>(a, grid, s); break;
-    case 10: launch_cfg<OP, 10, DBG>(a, grid, s); break;
-    case 11: launch_cfg<OP, 11, DBG>(a, grid, s); break;
-    case 12: launch_cfg<OP, 12, DBG>(a, grid, s); break;
-    default: launch_cfg<OP, 13, DBG>(a, grid, s); break;
+    case 0: launch_cfg<OP, 0, DBG, X8>(a, grid, s); break;
+    case 1: launch_cfg<OP, 1, DBG, X8>(a, grid, s); break;
+    case 2: launch_cfg<OP, 2, DBG, X8>(a, grid, s); break;
+    case 3: launch_cfg<OP, 3, DBG, X8>(a, grid, s); break;
+    case 4: launch_cfg<OP, 4, DBG, X8>(a, grid, s); break;
+    case 5: launch_cfg<OP, 5, DBG, X8>(a, grid, s); break;
+    case 6: launch_cfg<OP, 6, DBG, X8>(a, grid, s); break;
+    case 7: launch_cfg<OP, 7, DBG, X8>(a, grid, s); break;
+    case 8: launch_cfg<OP, 8, DBG, X8>(a, grid, s); break;
+    case 9: launch_cfg<OP, 9, DBG, X8>(a, grid, s); break;
+    case 10: launch_cfg<OP, 10, DBG, X8>(a, grid, s); break;
+    case 11: launch_cfg<OP, 11, DBG, X8>(a, grid, s); break;
+    case 12: launch_cfg<OP, 12, DBG, X8>(a, grid, s); break;
+    default: launch_cfg<OP, 13, DBG, X8>(a, grid, s); break;
   }
 }
 
 static int validate(const jr_conv_desc* d, int op, int dtype) {
-  if (dtype != JR_F32 && dtype != JR_BF16) return fail(JR_ERR_INVALID, "conv: bad dtype");
+  if (dtype != JR_F32 && dtype != JR_BF16 && dtype != JR_F32_X8) return fail(JR_ERR_INVALID, "conv: bad dtype");
   const int q = dtype == JR_BF16 ? 8 : 4;   // channels per 16 B piece
   if (!d) return fail(JR_ERR_INVALID, "conv: null descriptor");
   if (op < OP_FWD || op > OP_WGRAD) return fail(JR_ERR_INVALID, "conv: bad op");
@@ -674,6 +818,8 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     const TileCfg& t = kCfgsBf16[p.tile];
     const bool fast = OP == OP_WGRAD ? a.wo >= t.bk : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
     launch_conv_bf16(OP, p.tile, fast, a, grid, s);
+  } else if (dtype == JR_F32_X8) {
+    launch_op<OP, 0, true>(p.tile, a, grid, s);
   } else {
     launch_op<OP>(p.tile, a, grid, s);
   }
@@ -970,16 +1116,21 @@ JR_API int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const vo
   return autotune(d, op, dtype, a, b, c, ws, ws_bytes, stream, 3);
 }
 
-JR_API int jr_conv2d_num_configs(int dtype) { return dtype == JR_BF16 || dtype == JR_F32 ? cfg_count(dtype) : 0; }
+JR_API int jr_conv2d_num_configs(int dtype) {
+  return dtype == JR_BF16 || dtype == JR_F32 || dtype == JR_F32_X8 ? cfg_count(dtype) : 0;
+}
 
 // Diagnostic: time `reps` launches of one FWD GEMM (no split-K) of tile
-// config `cfg` in variant dbg (0 normal, 1 no MFMA, 2 no DMA, 3 no LDS
-// reads); returns ms via *ms.  Results of variants 1-3 are garbage.
+// config `cfg` in variant dbg (0 normal, 1 no MFMA, 2 no DMA, 3 no LDS reads;
+// +16 = the JR_F32_X8 kernel, whose variant 4 skips the operand split);
+// returns ms via *ms.  Results of variants other than 0 / 16 are garbage.
 JR_API int jr_conv2d_debug_time(const jr_conv_desc* d, int cfg, int dbg, const void* x, const void* w, void* y,
                                 int reps, float* ms, void* stream) {
   int rc = validate(d, OP_FWD, JR_F32);
   if (rc) return rc;
-  if (cfg < 0 || cfg >= kNumCfgs || dbg < 0 || dbg > 3) return fail(JR_ERR_INVALID, "debug_time: bad cfg/dbg");
+  const bool x8 = dbg >= 16;
+  if (x8) dbg -= 16;
+  if (cfg < 0 || cfg >= kNumCfgs || dbg < 0 || dbg > (x8 ? 4 : 3)) return fail(JR_ERR_INVALID, "debug_time: bad cfg/dbg");
   if (dbg > 0 && chan_pad(d->c_in, JR_F32) % kCfgs[cfg].bk != 0)
     return fail(JR_ERR_UNSUPPORTED, "debug_time: variants need c_in % BK == 0");
   ConvArgs a{};
@@ -996,11 +1147,16 @@ JR_API int jr_conv2d_debug_time(const jr_conv_desc* d, int cfg, int dbg, const v
   dim3 grid(p.mt * p.nt, 1, 1);
   (void)hipEventRecord(e0, s);
   for (int r = 0; r < reps; ++r) {
-    switch (dbg) {
+    switch (dbg + (x8 ? 16 : 0)) {
       case 0: launch_op<OP_FWD, 0>(cfg, a, grid, s); break;
       case 1: launch_op<OP_FWD, 1>(cfg, a, grid, s); break;
       case 2: launch_op<OP_FWD, 2>(cfg, a, grid, s); break;
-      default: launch_op<OP_FWD, 3>(cfg, a, grid, s); break;
+      case 3: launch_op<OP_FWD, 3>(cfg, a, grid, s); break;
+      case 16: launch_op<OP_FWD, 0, true>(cfg, a, grid, s); break;
+      case 17: launch_op<OP_FWD, 1, true>(cfg, a, grid, s); break;
+      case 18: launch_op<OP_FWD, 2, true>(cfg, a, grid, s); break;
+      case 19: launch_op<OP_FWD, 3, true>(cfg, a, grid, s); break;
+      default: launch_op<OP_FWD, 4, true>(cfg, a, grid, s); break;
     }
   }
   (void)hipEventRecord(e1, s);
@@ -1014,7 +1170,7 @@ JR_API int jr_conv2d_debug_time(const jr_conv_desc* d, int cfg, int dbg, const v
 JR_API int jr_conv2d_set_config(const jr_conv_desc* d, int op, int dtype, int phase, int cfg) {
   int rc = validate(d, op, dtype);
   if (rc) return rc;
-  if (cfg < 0 || cfg_tile(cfg) >= cfg_count(dtype) || cfg_splits(cfg) > 256)
+  if (cfg < -1 || (cfg >= 0 && (cfg_tile(cfg) >= cfg_count(dtype) || cfg_splits(cfg) > 256)))
     return fail(JR_ERR_INVALID, "conv set_config: bad config index");
   Phase ph[64];
   int nph = 1;
@@ -1025,7 +1181,10 @@ JR_API int jr_conv2d_set_config(const jr_conv_desc* d, int op, int dtype, int ph
   int M, N, K;
   gemm_dims(d, op, dtype, op == OP_DGRAD ? &ph[phase] : nullptr, &M, &N, &K);
   std::lock_guard<std::mutex> lk(g_tune_mu);
-  g_tuned[tune_key(dtype, op, M, N, K, d)] = cfg;
+  if (cfg < 0)
+    g_tuned.erase(tune_key(dtype, op, M, N, K, d));   // back to the planner's choice
+  else
+    g_tuned[tune_key(dtype, op, M, N, K, d)] = cfg;
   return JR_OK;
 }
 

@@ -41,15 +41,14 @@ template <typename T>
 __global__ void __launch_bounds__(256) k_maxpool_fwd(jr_pool_desc d, const T* __restrict__ x, T* y,
                                                      uint8_t* argmax) {
   const int c4 = d.c >> 2;
-  const int64_t total = (int64_t)d.n * d.ho * d.wo * c4;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(e % c4);
-    const int64_t pix = e / c4;
-    const int ow = (int)(pix % d.wo);
-    const int64_t t = pix / d.wo;
-    const int oh = (int)(t % d.ho);
-    const int b = (int)(t / d.ho);
+  const int total = d.n * d.ho * d.wo * c4;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int q = e % c4;
+    const int pix = e / c4;
+    const int ow = pix % d.wo;
+    const int t = pix / d.wo;
+    const int oh = t % d.ho;
+    const int b = t / d.ho;
     float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     int arg[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -64,11 +63,11 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(jr_pool_desc d, const T* __
           if (va[j] > best[j] || (r == 0 && c == 0)) { best[j] = va[j]; arg[j] = r * 3 + c; }
       }
     }
-    P4<T>::st(y + pix * d.y_c_stride + d.y_c_off + q * 4, make_float4(best[0], best[1], best[2], best[3]));
+    P4<T>::st(y + (int64_t)pix * d.y_c_stride + d.y_c_off + q * 4, make_float4(best[0], best[1], best[2], best[3]));
     if (argmax) {
       const uint32_t packed = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) |
                               ((uint32_t)arg[3] << 24);
-      *reinterpret_cast<uint32_t*>(argmax + pix * d.c + q * 4) = packed;
+      *reinterpret_cast<uint32_t*>(argmax + (int64_t)pix * d.c + q * 4) = packed;
     }
   }
 }
@@ -77,15 +76,14 @@ template <typename T>
 __global__ void __launch_bounds__(256) k_maxpool_bwd(jr_pool_desc d, const uint8_t* __restrict__ argmax,
                                                      const T* __restrict__ dy, T* dx, int accumulate) {
   const int c4 = d.c >> 2;
-  const int64_t total = (int64_t)d.n * d.h * d.w * c4;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(e % c4);
-    const int64_t pix = e / c4;
-    const int iw = (int)(pix % d.w);
-    const int64_t t = pix / d.w;
-    const int ih = (int)(t % d.h);
-    const int b = (int)(t / d.h);
+  const int total = d.n * d.h * d.w * c4;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int q = e % c4;
+    const int pix = e / c4;
+    const int iw = pix % d.w;
+    const int t = pix / d.w;
+    const int ih = t % d.h;
+    const int b = t / d.h;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     const int oh_lo = max(0, (ih - 1) / 2), oh_hi = min(d.ho - 1, ih / 2);
     const int ow_lo = max(0, (iw - 1) / 2), ow_hi = min(d.wo - 1, iw / 2);
@@ -101,7 +99,7 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(jr_pool_desc d, const uint8
           if ((int)((am >> (8 * j)) & 0xff) == pos) acc[j] += ga[j];
       }
     }
-    T* p = dx + pix * d.x_c_stride + d.x_c_off + q * 4;
+    T* p = dx + (int64_t)pix * d.x_c_stride + d.x_c_off + q * 4;
     float4 o = make_float4(acc[0], acc[1], acc[2], acc[3]);
     if (accumulate) o = f4add(o, P4<T>::ld(p));
     P4<T>::st(p, o);
@@ -111,15 +109,14 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(jr_pool_desc d, const uint8
 template <typename T>
 __global__ void __launch_bounds__(256) k_avgpool_fwd(jr_pool_desc d, const T* __restrict__ x, T* y) {
   const int c4 = d.c >> 2;
-  const int64_t total = (int64_t)d.n * d.ho * d.wo * c4;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(e % c4);
-    const int64_t pix = e / c4;
-    const int ow = (int)(pix % d.wo);
-    const int64_t t = pix / d.wo;
-    const int oh = (int)(t % d.ho);
-    const int b = (int)(t / d.ho);
+  const int total = d.n * d.ho * d.wo * c4;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int q = e % c4;
+    const int pix = e / c4;
+    const int ow = pix % d.wo;
+    const int t = pix / d.wo;
+    const int oh = t % d.ho;
+    const int b = t / d.ho;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     int cnt = 0;
     for (int r = -1; r <= 1; ++r) {
@@ -133,7 +130,7 @@ __global__ void __launch_bounds__(256) k_avgpool_fwd(jr_pool_desc d, const T* __
       }
     }
     const float fc = (float)cnt;
-    P4<T>::st(y + pix * d.y_c_stride + d.y_c_off + q * 4, make_float4(s.x / fc, s.y / fc, s.z / fc, s.w / fc));
+    P4<T>::st(y + (int64_t)pix * d.y_c_stride + d.y_c_off + q * 4, make_float4(s.x / fc, s.y / fc, s.z / fc, s.w / fc));
   }
 }
 
@@ -141,15 +138,14 @@ template <typename T>
 __global__ void __launch_bounds__(256) k_avgpool_bwd(jr_pool_desc d, const T* __restrict__ dy, T* dx,
                                                      int accumulate) {
   const int c4 = d.c >> 2;
-  const int64_t total = (int64_t)d.n * d.h * d.w * c4;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(e % c4);
-    const int64_t pix = e / c4;
-    const int iw = (int)(pix % d.w);
-    const int64_t t = pix / d.w;
-    const int ih = (int)(t % d.h);
-    const int b = (int)(t / d.h);
+  const int total = d.n * d.h * d.w * c4;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int q = e % c4;
+    const int pix = e / c4;
+    const int iw = pix % d.w;
+    const int t = pix / d.w;
+    const int ih = t % d.h;
+    const int b = t / d.h;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int r = -1; r <= 1; ++r) {
       const int oh = ih + r;
@@ -164,7 +160,7 @@ __global__ void __launch_bounds__(256) k_avgpool_bwd(jr_pool_desc d, const T* __
         s = f4add(s, make_float4(g.x / fc, g.y / fc, g.z / fc, g.w / fc));
       }
     }
-    T* p = dx + pix * d.x_c_stride + d.x_c_off + q * 4;
+    T* p = dx + (int64_t)pix * d.x_c_stride + d.x_c_off + q * 4;
     if (accumulate) s = f4add(s, P4<T>::ld(p));
     P4<T>::st(p, s);
   }
@@ -186,15 +182,14 @@ __global__ void k_gap_fwd(const T* __restrict__ x, int n, int hw, int c, float* 
 template <typename T>
 __global__ void k_gap_bwd(const float* __restrict__ dy, int n, int hw, int c, T* dx) {
   const int c4 = c >> 2;
-  const int64_t total = (int64_t)n * hw * c4;
+  const int total = n * hw * c4;
   const float f = (float)hw;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(e % c4);
-    const int64_t pix = e / c4;
-    const int b = (int)(pix / hw);
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int q = e % c4;
+    const int pix = e / c4;
+    const int b = pix / hw;
     const float4 g = *reinterpret_cast<const float4*>(dy + (int64_t)b * c + q * 4);
-    P4<T>::st(dx + pix * c + q * 4, make_float4(g.x / f, g.y / f, g.z / f, g.w / f));
+    P4<T>::st(dx + (int64_t)pix * c + q * 4, make_float4(g.x / f, g.y / f, g.z / f, g.w / f));
   }
 }
 
@@ -211,6 +206,10 @@ static int check_pool(const jr_pool_desc* d, int dtype, bool maxpool) {
     return fail(JR_ERR_INVALID, "pool: channels, offsets and strides must be multiples of 4");
   if (d->x_c_off < 0 || d->x_c_off + d->c > d->x_c_stride || d->y_c_off < 0 || d->y_c_off + d->c > d->y_c_stride)
     return fail(JR_ERR_INVALID, "pool: channel slice out of range");
+  // element indices (pixel x channel quad) are 32-bit in the kernels: the
+  // 64-bit divisions they replaced dominated the avgpool backward
+  if ((int64_t)d->n * d->h * d->w * (d->c / 4) >= (1LL << 30))
+    return fail(JR_ERR_UNSUPPORTED, "pool: more than 2^30 channel quads");
   if (maxpool) {
     if (d->h < 3 || d->w < 3 || d->ho != (d->h - 3) / 2 + 1 || d->wo != (d->w - 3) / 2 + 1)
       return fail(JR_ERR_INVALID, "maxpool: ho/wo must be (h-3)/2+1 (3x3 stride 2 valid)");
@@ -298,6 +297,7 @@ JR_API int jr_gap_fwd(int dtype, const void* x, int32_t n, int32_t hw, int32_t c
 
 JR_API int jr_gap_bwd(int dtype, const float* dy, int32_t n, int32_t hw, int32_t c, void* dx, void* stream) {
   if (!dy || !dx || n <= 0 || hw <= 0 || c <= 0 || c % 4) return fail(JR_ERR_INVALID, "gap_bwd: bad arguments");
+  if ((int64_t)n * hw * (c / 4) >= (1LL << 30)) return fail(JR_ERR_UNSUPPORTED, "gap_bwd: more than 2^30 channel quads");
   const int g = grid_for((int64_t)n * hw * (c / 4));
   if (dtype == JR_F32)
     hipLaunchKernelGGL(k_gap_bwd<float>, dim3(g), dim3(256), 0, as_stream(stream), dy, n, hw, c, (float*)dx);

@@ -52,6 +52,9 @@ def build_parser():
                    help="path to where operating points metrics should be saved")
     p.add_argument("-b", "--batch_size", default=DEFAULT_BATCH_SIZE, help="batch size")
     p.add_argument("-op", "--operating_threshold", default=0.5, help="operating threshold")
+    p.add_argument("--conv_math", default="x8", choices=["x8", "f32"],
+                   help="fp32 convolution arithmetic: x8 = exact 3-way bf16 split on the matrix cores (fp32-accurate, "
+                        "default), f32 = fp32 MFMA")
     return p
 
 
@@ -152,7 +155,7 @@ Using operating treshold: {},
     thresholds = lib.metrics.generate_thresholds(NUM_THRESHOLDS, KEPSILON) + [operating_threshold]
     _, meta = checkpoint.load(load_model_paths[0])
     engine = Engine(batch_size, meta["height"], meta["width"], meta.get("units", 1), device=local,
-                    train=False)
+                    train=False, conv_math=args.conv_math)
     preds, labels, order = predict_all(engine, load_model_paths, data_dir, batch_size, rank, world)
 
     if dist:   # gather every rank's batches to rank 0, restore dataset order

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("JR_LIB", os.path.join(_HERE, "libjr.so"))
 JR_OK = 0
 JR_F32 = 0
 JR_BF16 = 1
+JR_F32_X8 = 2      # conv entry points only: fp32 tensors, bf16x8-split MFMA products (jr.h)
 JR_CONV_FWD, JR_CONV_BWD_DATA, JR_CONV_BWD_FILTER = 0, 1, 2
 JR_HEAD_SIGMOID, JR_HEAD_SOFTMAX = 0, 1
 

@@ -46,9 +46,15 @@ class Engine:
                  device: int | torch.device = 0, dtype: str = "f32", train: bool = True,
                  optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
                  head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None,
-                 autotune: bool = True, fuse_siblings: bool = True, lanes: int = 2):
+                 autotune: bool = True, fuse_siblings: bool = True, lanes: int = 2,
+                 conv_math: Optional[str] = None):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
+        if conv_math is None:            # fp32 default: x8 (fp32-accurate, on the bf16 matrix cores)
+            conv_math = "x8" if dtype == "f32" else "bf16"
+        if (dtype == "f32" and conv_math not in ("f32", "x8")) or (dtype == "bf16" and conv_math != "bf16"):
+            raise ValueError("conv_math: 'x8' or 'f32' for dtype f32 (x8 = JR_F32_X8, f32 = fp32 MFMA); "
+                             "'bf16' for dtype bf16")
         if not torch.cuda.is_available():
             raise RuntimeError("jr.Engine needs a ROCm GPU (libjr has no CPU path)")
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
@@ -58,6 +64,11 @@ class Engine:
         self.batch = batch
         self.dt = DTYPES[dtype]
         self.dtype = dtype
+        # dtype code of the convolution calls: JR_F32_X8 keeps every tensor
+        # fp32 and forms the GEMM products on the bf16 matrix cores from an
+        # exact three-way split (jr.h); everything else runs self.dt
+        self.conv_math = conv_math
+        self.cdt = _ffi.JR_F32_X8 if conv_math == "x8" else self.dt
         self.train_mode = train
         self.optimizer = optimizer
         self.lr = float(lr)
@@ -146,7 +157,7 @@ class Engine:
             d = self._conv_desc(u, B)
             ops = (_ffi.JR_CONV_FWD, _ffi.JR_CONV_BWD_DATA, _ffi.JR_CONV_BWD_FILTER)
             for op in (ops if self.train_mode else ops[:1]):
-                ws = max(ws, self.lib.jr_conv2d_workspace_size(ctypes.byref(d), op, self.dt))
+                ws = max(ws, self.lib.jr_conv2d_workspace_size(ctypes.byref(d), op, self.cdt))
             for n in u.members:
                 ws = max(ws, self.lib.jr_bn_workspace_size(B * n.ho * n.wo, n.cout))
         self.ws_bytes = int(ws)
@@ -208,16 +219,16 @@ class Engine:
             d = self._conv_desc(u, B)
             x = self.acts[u.x].data_ptr()
             raw = self.raw_unit[u.first.idx].data_ptr()
-            _ffi.check("autotune fwd", L.jr_conv2d_autotune(ctypes.byref(d), _ffi.JR_CONV_FWD, self.dt, x,
+            _ffi.check("autotune fwd", L.jr_conv2d_autotune(ctypes.byref(d), _ffi.JR_CONV_FWD, self.cdt, x,
                                                              self._wf(u), raw, ws, wsb, s))
             if not self.train_mode:
                 continue
             _ffi.check("autotune wgrad", L.jr_conv2d_autotune(
-                ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, self.dt, x, self.draw.data_ptr(),
+                ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, self.cdt, x, self.draw.data_ptr(),
                 self.grads.data_ptr() + 4 * u.koff, ws, wsb, s))
             if u.x != self.g.input_buf:
                 _ffi.check("autotune dgrad", L.jr_conv2d_autotune(
-                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.dt, self.draw.data_ptr(), self._wd(u),
+                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.cdt, self.draw.data_ptr(), self._wd(u),
                     self.dacts[u.x].data_ptr(), ws, wsb, s))
         self.synchronize()
         if self.train_mode:
@@ -228,9 +239,9 @@ class Engine:
         out = {}
         for u in self.cunits:
             d = self._conv_desc(u, self.batch)
-            f = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_FWD, self.dt, 0)
-            wg = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, self.dt, 0)
-            dg = [self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.dt, p)
+            f = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_FWD, self.cdt, 0)
+            wg = self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, self.cdt, 0)
+            dg = [self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.cdt, p)
                   for p in range(u.stride * u.stride)]
             out[u.name] = (f, wg, dg)
         return out
@@ -282,7 +293,7 @@ class Engine:
             return self._calls[key]
         if B > self.batch or B <= 0:
             raise ValueError(f"batch {B} outside 1..{self.batch}")
-        L, g, dt = self.lib, self.g, self.dt
+        L, g, dt, cdt = self.lib, self.g, self.dt, self.cdt
         S = [ctypes.c_void_p(st.cuda_stream) for st in self.lane_streams[:nl]]
         if one_stream:
             S = [S[0]] * nl
@@ -321,7 +332,7 @@ class Engine:
                 uid = u.first.idx
                 raw = self.raw_unit[uid].data_ptr()
                 # conv + the BN batch statistics of its raw output, fused
-                add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), dt, A(u.x), self._wf(u), raw, BN_EPS,
+                add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), cdt, A(u.x), self._wf(u), raw, BN_EPS,
                                                     self.mean_unit[uid].data_ptr(),
                                                     self.invstd_unit[uid].data_ptr(), ws, wsb, s),
                     "conv_fwd", ln, a_all(u.x) + [wkey], [("r", uid), ("ws", ln)])
@@ -382,11 +393,11 @@ class Engine:
                                                     self._gp(f"batch_normalization_{m.idx + 1}/beta"), ws, wsb, s),
                             "bn_relu_bwd", ln, [("d", m.y.buf, m.y.c_off), ("r", uid), ("p",)],
                             [("draw", ln), ("g", uid), ("ws", ln)])
-                    add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), dt, A(u.x), draw,
+                    add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), cdt, A(u.x), draw,
                                                       self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
                         "conv_wgrad", ln, a_all(u.x) + [("draw", ln)], [("g", uid), ("ws", ln)])
                     if u.x != g.input_buf:
-                        add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), dt, draw, self._wd(u), D(u.x), acc, ws, wsb,
+                        add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), cdt, draw, self._wd(u), D(u.x), acc, ws, wsb,
                                                         s),
                             "conv_dgrad", ln, [("draw", ln), wkey], d_all(u.x) + [("ws", ln)])
                         written.add(u.x)

@@ -68,6 +68,9 @@ def build_parser():
     p.add_argument("--image_size", type=int, default=299, help="input resolution (299; 587 high-res variant)")
     p.add_argument("--num_epochs", type=int, default=NUM_EPOCHS)
     p.add_argument("--seed", type=int, default=0, help="weight init seed (ensemble member index)")
+    p.add_argument("--conv_math", default="x8", choices=["x8", "f32"],
+                   help="fp32 convolution arithmetic: x8 = exact 3-way bf16 split on the matrix cores (fp32-accurate, "
+                        "default), f32 = fp32 MFMA")
     p.add_argument("--shuffle_seed", type=int, default=None)
     p.add_argument("--max_steps_per_epoch", type=int, default=None)
     return p
@@ -134,7 +137,7 @@ Use SGD: {bool(args.vanilla_sgd)}
 
     engine = Engine(max(TRAIN_BATCH_SIZE, VAL_BATCH_SIZE), args.image_size, args.image_size,
                     device=local, optimizer="sgd" if args.vanilla_sgd else ("nesterov" if USE_NESTEROV else "momentum"),
-                    lr=LEARNING_RATE, momentum=MOMENTUM, seed=args.seed)
+                    lr=LEARNING_RATE, momentum=MOMENTUM, seed=args.seed, conv_math=args.conv_math)
     sess = Session(engine, thresholds, NUM_THRESHOLDS, KEPSILON)
     if dist:
         from jr.dist import BucketAllReduce

@@ -20,8 +20,8 @@ def _grad_errors(grads, grads_ref):
     return out
 
 
-@pytest.mark.parametrize("res,batch", [(107, 3), (139, 2)])
-def test_forward_and_one_step_match_oracle(res, batch):
+@pytest.mark.parametrize("res,batch,math", [(107, 3, "f32"), (139, 2, "f32"), (107, 3, "x8")])
+def test_forward_and_one_step_match_oracle(res, batch, math):
     """Forward logits within the north-star 1e-3; gradients and the updated
     weights within a few x the error of an fp32 CPU implementation of the same
     graph (the backward of this BN-heavy net amplifies fp32 rounding to ~1e-2
@@ -31,7 +31,7 @@ def test_forward_and_one_step_match_oracle(res, batch):
     from jr import synth
     from oracle.inception_ref import InceptionV3Ref
 
-    eng = Engine(batch, res, res, seed=1)
+    eng = Engine(batch, res, res, seed=1, conv_math=math)
     imgs = synth.fundus_batch(0, batch, res)
     y = np.array([[1.0], [0.0], [1.0]][:batch], np.float32)
     eng.set_batch(imgs, y)

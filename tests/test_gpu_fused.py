@@ -44,15 +44,16 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype", ["f32", "f32x8", "bf16"])
 @pytest.mark.parametrize("case", CASES)
 def test_conv_fwd_bn_stats(case, dtype):
     from jr import _ffi
     _ffi.init(0)
     L = _ffi.load()
-    dt = 0 if dtype == "f32" else 1
-    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
-    q = 4 if dtype == "f32" else 8
+    dt = {"f32": 0, "bf16": 1, "f32x8": 2}[dtype]
+    f32 = dtype != "bf16"
+    tdt = torch.float32 if f32 else torch.bfloat16
+    q = 4 if f32 else 8
     n, h, w, cin, cout, kh, kw, s, pad = case
     rng = np.random.default_rng(sum(case[:8]))
     x = rng.standard_normal((n, h, w, cin)) + 0.5        # non-zero mean: exercises the centred M2
@@ -62,7 +63,7 @@ def test_conv_fwd_bn_stats(case, dtype):
     xp[..., :cin] = x
     X = _t(xp, tdt)
     xr = X.double().cpu().numpy()[..., :cin]               # the input as the kernel sees it
-    if dtype == "f32":
+    if f32:
         W = _t(wt, torch.float32)
         wr = wt.astype(np.float64)
     else:
@@ -79,7 +80,7 @@ def test_conv_fwd_bn_stats(case, dtype):
     wsb = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, dt) + 5 * n * ho * wo * cout * 4 + (1 << 20)
     ws = torch.zeros(wsb // 4 + 4, device="cuda")
     _KEEP.append(ws)
-    for cfg in (None, 0 | (1 << 8), 0 | (3 << 8), 3 | (1 << 8), 3 | (5 << 8)):
+    for cfg in (None, 0 | (1 << 8), 0 | (3 << 8), 3 | (1 << 8), 3 | (5 << 8), -1):
         if cfg is not None:
             _ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, dt, 0, cfg))
         Y = torch.zeros(n * ho * wo * cout, dtype=tdt, device="cuda")
@@ -92,7 +93,7 @@ def test_conv_fwd_bn_stats(case, dtype):
         torch.cuda.synchronize()
         y = Y.double().cpu().numpy().reshape(ref.shape)
         scale = np.abs(ref).max()
-        tol = 1e-5 if dtype == "f32" else 8e-3
+        tol = 1e-5 if f32 else 8e-3
         assert np.abs(y - ref).max() <= tol * scale, (cfg, np.abs(y - ref).max() / scale)
         yf = y.reshape(-1, cout)
         mu = yf.mean(0)

@@ -71,13 +71,19 @@ def _desc(ffi, n, h, w, cin, cout, kh, kw, s, pad, x_off=0, x_stride=None, y_off
                         y_off, y_stride or cout), ho, wo
 
 
-def _ws(ffi, d, op):
-    b = ffi.load().jr_conv2d_workspace_size(ctypes.byref(d), op, 0)
+def _ws(ffi, d, op, dt=0):
+    b = ffi.load().jr_conv2d_workspace_size(ctypes.byref(d), op, dt)
     return torch.zeros(max(b // 4, 1) + 4, device="cuda"), b
 
 
+# conv dtype codes: 0 = JR_F32 (fp32 MFMA), 2 = JR_F32_X8 (fp32 tensors, products
+# from the exact three-way bf16 split) -- held to the SAME fp32 tolerances
+CONV_DT = [pytest.param(0, id="f32"), pytest.param(2, id="f32x8")]
+
+
+@pytest.mark.parametrize("dt", CONV_DT)
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_dgrad_wgrad(case):
+def test_conv_fwd_dgrad_wgrad(case, dt):
     ffi = _lib()
     L = ffi.load()
     n, h, w, cin, cout, kh, kw, s, pad = case
@@ -91,8 +97,8 @@ def test_conv_fwd_dgrad_wgrad(case):
     xp[..., :cin] = x
     X, W = dev(xp), dev(wt)
     Y = torch.zeros(n * ho * wo * cout, device="cuda")
-    ws, wsb = _ws(ffi, d, 0)
-    ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), 0, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
+    ws, wsb = _ws(ffi, d, 0, dt)
+    ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), dt, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
                                      ws.data_ptr(), wsb, None))
     got = host(Y).reshape(ref.shape)
     assert relerr(got, ref) < 5e-6, relerr(got, ref)
@@ -102,28 +108,29 @@ def test_conv_fwd_dgrad_wgrad(case):
     if cin % 4 == 0 and cout % 16 == 0:
         ref_dx = R.conv2d_bwd_data(dy, wt, x.shape, s, pad)
         DX = torch.zeros(x.size, device="cuda")
-        ws, wsb = _ws(ffi, d, 1)
-        ffi.check("dgrad", L.jr_conv2d_bwd_data(ctypes.byref(d), 0, DY.data_ptr(), W.data_ptr(), DX.data_ptr(),
+        ws, wsb = _ws(ffi, d, 1, dt)
+        ffi.check("dgrad", L.jr_conv2d_bwd_data(ctypes.byref(d), dt, DY.data_ptr(), W.data_ptr(), DX.data_ptr(),
                                                 0, ws.data_ptr(), wsb, None))
         got = host(DX).reshape(x.shape)
         assert relerr(got, ref_dx) < 5e-6, relerr(got, ref_dx)
         # accumulate = 1 adds into the existing gradient
-        ffi.check("dgrad acc", L.jr_conv2d_bwd_data(ctypes.byref(d), 0, DY.data_ptr(), W.data_ptr(),
+        ffi.check("dgrad acc", L.jr_conv2d_bwd_data(ctypes.byref(d), dt, DY.data_ptr(), W.data_ptr(),
                                                     DX.data_ptr(), 1, ws.data_ptr(), wsb, None))
         got = host(DX).reshape(x.shape)
         assert relerr(got, 2 * ref_dx) < 5e-6
     ref_dw = R.conv2d_bwd_filter(x, dy, wt.shape, s, pad)
     DW = torch.zeros(wt.size, device="cuda")
-    ws, wsb = _ws(ffi, d, 2)
-    ffi.check("wgrad", L.jr_conv2d_bwd_filter(ctypes.byref(d), 0, X.data_ptr(), DY.data_ptr(), DW.data_ptr(),
+    ws, wsb = _ws(ffi, d, 2, dt)
+    ffi.check("wgrad", L.jr_conv2d_bwd_filter(ctypes.byref(d), dt, X.data_ptr(), DY.data_ptr(), DW.data_ptr(),
                                               ws.data_ptr(), wsb, None))
     got = host(DW).reshape(wt.shape)
     assert relerr(got, ref_dw) < 1e-5, relerr(got, ref_dw)
 
 
+@pytest.mark.parametrize("dt", CONV_DT)
 @pytest.mark.parametrize("case", [(2, 17, 17, 64, 96, 3, 3, 1, "same"), (2, 17, 17, 48, 64, 3, 3, 2, "valid"),
                                   (2, 11, 11, 3, 32, 3, 3, 2, "valid")])
-def test_conv_every_tile_config(case):
+def test_conv_every_tile_config(case, dt):
     """Every tile configuration the autotuner may pick is correct, with the
     planner's split-K factor and with forced factors (id = tile | splits << 8)."""
     ffi = _lib()
@@ -141,28 +148,71 @@ def test_conv_every_tile_config(case):
     ref_dx = R.conv2d_bwd_data(dy, wt, x.shape, s, pad) if cin % 4 == 0 else None
     ref_dw = R.conv2d_bwd_filter(x, dy, wt.shape, s, pad)
     X, W, DY = dev(xp), dev(wt), dev(dy)
-    wsb = max(L.jr_conv2d_workspace_size(ctypes.byref(d), op, 0) for op in range(3))
+    wsb = max(L.jr_conv2d_workspace_size(ctypes.byref(d), op, dt) for op in range(3))
     wsb += 3 * 4 * max(n * ho * wo * cout, kh * kw * cs * cout, n * h * w * cs)   # forced splits of 3
     ws = torch.zeros(wsb // 4 + 4, device="cuda")
-    cfgs = [t | (sp << 8) for t in range(L.jr_conv2d_num_configs(0)) for sp in (0, 1, 3)]  # forced split-K
+    cfgs = [t | (sp << 8) for t in range(L.jr_conv2d_num_configs(dt)) for sp in (0, 1, 3)]  # forced split-K
     for cfg in cfgs:
-        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, 0, 0, cfg))
-        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 2, 0, 0, cfg))
+        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, dt, 0, cfg))
+        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 2, dt, 0, cfg))
         Y = torch.zeros(ref.size, device="cuda")
-        ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), 0, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
+        ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), dt, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
                                          ws.data_ptr(), wsb, None))
         assert relerr(host(Y).reshape(ref.shape), ref) < 5e-6, cfg
         DW = torch.zeros(wt.size, device="cuda")
-        ffi.check("wgrad", L.jr_conv2d_bwd_filter(ctypes.byref(d), 0, X.data_ptr(), DY.data_ptr(), DW.data_ptr(),
+        ffi.check("wgrad", L.jr_conv2d_bwd_filter(ctypes.byref(d), dt, X.data_ptr(), DY.data_ptr(), DW.data_ptr(),
                                                   ws.data_ptr(), wsb, None))
         assert relerr(host(DW).reshape(wt.shape), ref_dw) < 1e-5, cfg
         if ref_dx is not None:
             for ph in range(s * s):
-                ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 1, 0, ph, cfg))
+                ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 1, dt, ph, cfg))
             DX = torch.zeros(x.size, device="cuda")
-            ffi.check("dgrad", L.jr_conv2d_bwd_data(ctypes.byref(d), 0, DY.data_ptr(), W.data_ptr(), DX.data_ptr(),
+            ffi.check("dgrad", L.jr_conv2d_bwd_data(ctypes.byref(d), dt, DY.data_ptr(), W.data_ptr(), DX.data_ptr(),
                                                     0, ws.data_ptr(), wsb, None))
             assert relerr(host(DX).reshape(x.shape), ref_dx) < 5e-6, cfg
+    for op in (0, 2):                    # drop the overrides: later tests get the planner's choice
+        ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), op, dt, 0, -1))
+    if ref_dx is not None:
+        for ph in range(s * s):
+            ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 1, dt, ph, -1))
+
+
+@pytest.mark.parametrize("case", [(4, 8, 8, 2048, 384, 1, 1, 1, "same"), (4, 17, 17, 192, 192, 7, 1, 1, "same"),
+                                  (2, 35, 35, 288, 384, 3, 3, 2, "valid")])
+def test_conv_x8_error_matches_fp32(case):
+    """JR_F32_X8 is fp32 arithmetic, not reduced precision: on long
+    reductions (K up to 2,592) its max error against the fp64 oracle stays
+    within 2x the native fp32-MFMA kernel's, for fwd, dgrad and wgrad."""
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, cin, cout, kh, kw, s, pad = case
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
+    wt = (rng.standard_normal((kh, kw, cin, cout)) / np.sqrt(kh * kw * cin)).astype(np.float32)
+    d, ho, wo = _desc(ffi, n, h, w, cin, cout, kh, kw, s, pad)
+    ref = R.conv2d(x, wt, s, pad)
+    dy = rng.standard_normal(ref.shape).astype(np.float32)
+    ref_dx = R.conv2d_bwd_data(dy, wt, x.shape, s, pad)
+    ref_dw = R.conv2d_bwd_filter(x, dy, wt.shape, s, pad)
+    X, W, DY = dev(x), dev(wt), dev(dy)
+    err = {}
+    for dt in (0, 2):
+        Y = torch.zeros(ref.size, device="cuda")
+        DX = torch.zeros(x.size, device="cuda")
+        DW = torch.zeros(wt.size, device="cuda")
+        ws, wsb = _ws(ffi, d, 0, dt)
+        ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), dt, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
+                                         ws.data_ptr(), wsb, None))
+        ws, wsb = _ws(ffi, d, 1, dt)
+        ffi.check("dgrad", L.jr_conv2d_bwd_data(ctypes.byref(d), dt, DY.data_ptr(), W.data_ptr(), DX.data_ptr(),
+                                                0, ws.data_ptr(), wsb, None))
+        ws, wsb = _ws(ffi, d, 2, dt)
+        ffi.check("wgrad", L.jr_conv2d_bwd_filter(ctypes.byref(d), dt, X.data_ptr(), DY.data_ptr(), DW.data_ptr(),
+                                                  ws.data_ptr(), wsb, None))
+        err[dt] = (relerr(host(Y).reshape(ref.shape), ref), relerr(host(DX).reshape(x.shape), ref_dx),
+                   relerr(host(DW).reshape(wt.shape), ref_dw))
+    for e32, ex8 in zip(err[0], err[2]):
+        assert ex8 <= 2.0 * e32 + 2e-7, err
 
 
 def test_conv_channel_slices():
