@@ -95,16 +95,18 @@ def conv_roofline(eng, steps: int = 3):
     return flops, t, len(pairs) // steps
 
 
-def pmc_traffic(dtype: str, B: int, res: int) -> dict:
+def pmc_traffic(dtype: str, B: int, res: int, math: str = "x8") -> dict:
     """HBM bytes of the conv family per training step from the committed
     rocprofv3 PMC summary of the same workload (tools/pmc_step.sh ->
     profiles/r01_pmc_<dtype>.json: FETCH_SIZE x 2 (gfx950 tallies 128-B
     requests at 64 B, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, over the
-    conv GEMM, split-K reduce and statistics kernels of one step).  bench.py
+    conv GEMM, split-K reduce and statistics kernels of one step; the fp32
+    MFMA variant's summary is r01_pmc_f32mfma.json).  bench.py
     cannot run the profiler itself, so `traffic` is null without that file."""
     if (B, res) != (64, 299):
         return {}
-    p = os.path.join(ROOT, "profiles", f"r01_pmc_{dtype}.json")
+    tag = "f32mfma" if (dtype == "f32" and math == "f32") else dtype
+    p = os.path.join(ROOT, "profiles", f"r01_pmc_{tag}.json")
     if not os.path.exists(p):
         return {}
     fam = json.load(open(p))["families"].get("conv", {})
@@ -220,7 +222,7 @@ def main():
                     "conv_ms_per_step": round(tconv * 1e3, 3),
                     "algorithmic_gflop_per_step": round(flops / 1e9, 1)}
             if train:
-                roof.update(pmc_traffic(args.dtype, B, res))
+                roof.update(pmc_traffic(args.dtype, B, res, math))
         out = {
             "metric": (f"train images/sec, Inception-v3 {res}^2 bs{B}/GPU" if train else
                        f"eval images/sec, Inception-v3 {res}^2 bs{B}/GPU (one ensemble member, batch-stat BN)"),
