@@ -442,13 +442,17 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       // MFMAs accumulate the partial products in fp32 (SplitFrag).
       constexpr int G8 = HALF / 8;
       static_assert(HALF % 8 == 0, "X8 needs BK % 16 == 0");
-      // Three MFMA phases per 16-k group, each a scheduling region closed by
-      // a DMA piece (the LDS-DMA intrinsic is a scheduling boundary), each
-      // carrying the VALU the NEXT phase needs so the split hides under MFMAs:
-      //   P1: h packs (cheap: one cvt per pair) | hh MFMAs + residuals, m packs
-      //   P2: hm mh mm MFMAs + second residuals, l packs
-      //   P3: hl lh (ml lm) MFMAs
-      // Terms are added largest first.
+      // Five MFMA phases per 16-k group, each a scheduling region carrying
+      // the split VALU the NEXT phase needs, so the split issues under MFMAs
+      // and every region holds about as much VALU as its MFMAs can cover:
+      //   (h packs: one cvt per pair)
+      //   P1: hh        | A residuals, A m packs
+      //   P2: mh        | B residuals, B m packs
+      //   P3: hm mm     | A second residuals, A l packs
+      //   P4: lh        | B second residuals, B l packs
+      //   P5: hl (ml lm)
+      // (three phases -- hh | all m; hm mh mm | all l; the rest -- left the
+      // first one VALU-bound and the last one VALU-idle).
       int piece = 0;
       auto next_piece = [&]() {
         if constexpr (DO_ISSUE && DBG != 2) {
@@ -471,34 +475,46 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
         for (int i = 0; i < TM; ++i) sa[i].init(&af[i][8 * g8], DBG == 4);
 #pragma unroll
         for (int j = 0; j < TN; ++j) sb[j].init(&bfr[j][8 * g8], DBG == 4);
+        // (sched_barrier closes each region even when this wave has no DMA
+        // piece left to issue)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) mma(i, j, sa[i].h(), sb[j].h());
 #pragma unroll
         for (int i = 0; i < TM; ++i) sa[i].stage2(DBG == 4);
+        next_piece();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) mma(i, j, sa[i].m(), sb[j].h());
 #pragma unroll
         for (int j = 0; j < TN; ++j) sb[j].stage2(DBG == 4);
-        next_piece();
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             mma(i, j, sa[i].h(), sb[j].m());
-            mma(i, j, sa[i].m(), sb[j].h());
             mma(i, j, sa[i].m(), sb[j].m());
           }
 #pragma unroll
         for (int i = 0; i < TM; ++i) sa[i].stage3(DBG == 4);
+        next_piece();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) mma(i, j, sa[i].l(), sb[j].h());
 #pragma unroll
         for (int j = 0; j < TN; ++j) sb[j].stage3(DBG == 4);
-        next_piece();
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             mma(i, j, sa[i].h(), sb[j].l());
-            mma(i, j, sa[i].l(), sb[j].h());
             if constexpr (kSplitTerms == 8) {
               mma(i, j, sa[i].m(), sb[j].l());
               mma(i, j, sa[i].l(), sb[j].m());
