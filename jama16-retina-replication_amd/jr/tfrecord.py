@@ -28,16 +28,22 @@ FeatureValue = Union[bytes, int, float, List[bytes], List[int], List[float], np.
 
 
 # ------------------------------------------------------------------ CRC32C
+def _ptr(data) -> bytes:
+    # a bytes object is passed to the C-ABI as a pointer to its own buffer
+    # (no copy: the record payloads are ~80 KB JPEGs, read once per record)
+    return data if isinstance(data, bytes) else bytes(data)
+
+
 def masked_crc32c(data: bytes) -> int:
     lib = _ffi.load()
-    buf = ctypes.create_string_buffer(bytes(data), len(data))
-    return int(lib.jr_masked_crc32c(buf, len(data)))
+    b = _ptr(data)
+    return int(lib.jr_masked_crc32c(b, len(b)))
 
 
 def crc32c(data: bytes, crc: int = 0) -> int:
     lib = _ffi.load()
-    buf = ctypes.create_string_buffer(bytes(data), len(data))
-    return int(lib.jr_crc32c(buf, len(data), crc))
+    b = _ptr(data)
+    return int(lib.jr_crc32c(b, len(b), crc))
 
 
 # --------------------------------------------------------------- container
