@@ -147,12 +147,21 @@ def main():
     if world != args.gpus:
         if rank == 0 and world > 1:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # rehearsal knobs for the N>1 path on a one-GPU box (not for measurement):
+    # JR_BENCH_ONE_DEVICE=1 puts every rank on cuda:0, JR_DIST_BACKEND=gloo
+    # replaces RCCL (which refuses two ranks on one device)
+    if os.environ.get("JR_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("JR_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from jr.engine import Engine
     from jr import synth
