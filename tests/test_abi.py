@@ -43,6 +43,14 @@ def test_validation_errors_without_gpu():
     d = _ffi.ConvDesc(1, 8, 8, 16, 24, 3, 3, 1, 1, 1, 1, 8, 8, 0, 16, 0, 24)
     assert L.jr_conv2d_fwd(ctypes.byref(d), 0, 16, 16, 16, None, 0, None) == -3   # c_out % 16
     assert L.jr_conv2d_workspace_size(None, 0, 0) == 0
+    # JR_F32_X8 (dtype 2): fp32 storage rules and tile table, conv entry points only
+    d = _ffi.ConvDesc(2, 17, 17, 64, 96, 3, 3, 1, 1, 1, 1, 17, 17, 0, 64, 0, 96)
+    assert L.jr_conv2d_num_configs(2) == L.jr_conv2d_num_configs(0) > 0
+    for op in range(3):
+        assert L.jr_conv2d_workspace_size(ctypes.byref(d), op, 2) == L.jr_conv2d_workspace_size(ctypes.byref(d), op, 0)
+    assert L.jr_conv2d_num_configs(3) == 0
+    assert L.jr_conv2d_fwd(ctypes.byref(d), 3, 16, 16, 16, None, 0, None) == -1      # bad dtype
+    assert L.jr_bn_relu_apply(2, 16, 0, 8, 10, 8, 16, 16, 16, 16, 0, 8, None) == -1   # x8 is conv-only
     assert L.jr_bn_relu_apply(0, 16, 0, 6, 10, 6, 16, 16, 16, 16, 0, 6, None) == -1   # c % 4
     assert L.jr_bn_relu_apply(0, 16, 4, 8, 10, 8, 16, 16, 16, 16, 0, 8, None) == -1   # x slice out of range
     assert L.jr_head_fwd(0, None, None, None, None, 1, 1, 1, None, None, None, None) == -1
