@@ -1,5 +1,7 @@
 // jr_conv.hip — Conv2D forward / data-grad / filter-grad as implicit GEMM on
-// gfx950 MFMA (fp32: v_mfma_f32_32x32x2_f32, exact f32 at the f32 peak rate).
+// gfx950 MFMA for fp32 tensors: JR_F32 on v_mfma_f32_32x32x2_f32 (exact f32
+// at the f32 peak rate), JR_F32_X8 on v_mfma_f32_32x32x16_bf16 through an
+// exact three-way bf16 split of the operands (SplitFrag; 2x the f32 peak).
 //
 // Replaces the TF ops behind the 94 Keras Conv2D(use_bias=False) layers that
 // train.py:129-130 instantiates, and their gradients created by .minimize at
