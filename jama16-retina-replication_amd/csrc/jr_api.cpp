@@ -28,7 +28,7 @@ using namespace jr;
 
 JR_API const char* jr_last_error(void) { return g_last_error.c_str(); }
 
-JR_API const char* jr_version(void) { return "libjr 0.1 gfx950 (fp32 MFMA implicit-GEMM conv)"; }
+JR_API const char* jr_version(void) { return "libjr 0.2 gfx950 (implicit-GEMM conv: fp32 x8-split / fp32 / bf16 MFMA)"; }
 
 JR_API int jr_init(int device) {
   int n = 0;
