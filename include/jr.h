@@ -226,10 +226,26 @@ int jr_image_u8_to_nhwc(const uint8_t* src, void* dst, int dtype, int64_t pixels
  * train.py:175-177) */
 int jr_brier_accumulate(const float* probs, const float* labels, int32_t n, double* acc, void* stream);
 
-/* ---- host (CPU) helpers: TFRecord container checksums -------------- */
+/* ---- host (CPU) helpers: TFRecord container and Example records ----- */
 uint32_t jr_crc32c(const uint8_t* data, size_t n, uint32_t crc);
 /* TFRecord masked CRC32C: ((c >> 15) | (c << 17)) + 0xa282ead8 */
 uint32_t jr_masked_crc32c(const uint8_t* data, size_t n);
+/* Index the records of one TFRecord file image in memory (replaces the
+ * record walk of tf.data.TFRecordDataset behind lib/dataset.py:5-8,44-47).
+ * Writes the payload offset/length of each record; stops at the first damaged
+ * record (truncated, or CRC mismatch when verify != 0) with *n_records = the
+ * good records before it and JR_ERR_INVALID.  offsets == NULL only counts. */
+int jr_tfrecord_index(const uint8_t* buf, size_t len, int verify, uint64_t* offsets, uint64_t* lengths,
+                      size_t cap, size_t* n_records);
+/* Locate the lib/dataset.py:12-16 FixedLenFeatures (image/encoded,
+ * image/format, image/class/label, image/height, image/width) in n serialized
+ * tf.train.Example records at base + offsets[i] (replaces the
+ * tf.parse_single_example of lib/dataset.py:17).  status[i]: 0 ok; > 0 bitmask
+ * of keys missing / not exactly one value / wrong list type (bit k = key k in
+ * the order above); -1 malformed protobuf.  enc_off is relative to base. */
+int jr_example_parse_image(const uint8_t* base, const uint64_t* offsets, const uint64_t* lengths, size_t n,
+                           uint64_t* enc_off, uint64_t* enc_len, int64_t* label, int64_t* height,
+                           int64_t* width, int32_t* status);
 
 /* ---- HIP graph capture of a whole step ------------------------------ */
 int jr_graph_begin(void* stream);

@@ -106,6 +106,9 @@ _SIGS = {
     "jr_brier_accumulate": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "jr_crc32c": (ctypes.c_uint32, [c_void_p, c_size_t, ctypes.c_uint32]),
     "jr_masked_crc32c": (ctypes.c_uint32, [c_void_p, c_size_t]),
+    "jr_tfrecord_index": (c_int, [c_void_p, c_size_t, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "jr_example_parse_image": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p]),
     "jr_graph_begin": (c_int, [c_void_p]),
     "jr_graph_end": (c_int, [c_void_p, POINTER(c_void_p)]),
     "jr_graph_get_deps": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),

@@ -17,6 +17,8 @@ Example:   protobuf  Example{1: Features{1: map<string, Feature>}}
 from __future__ import annotations
 
 import ctypes
+import mmap
+import os
 import struct
 from typing import Dict, Iterator, List, Union
 
@@ -71,6 +73,74 @@ def read_records(path: str, verify: bool = True) -> Iterator[bytes]:
             if verify and masked_crc32c(data) != struct.unpack("<I", tail)[0]:
                 raise TFRecordError(f"{path}: corrupted record data")
             yield data
+
+
+_KEYS = ("image/encoded", "image/format", "image/class/label", "image/height", "image/width")
+
+
+class RecordFile:
+    """One TFRecord file, mmap'd and indexed by libjr (jr_tfrecord_index), with
+    the lib/dataset.py:12-16 features of every record located natively
+    (jr_example_parse_image).  Records past a damaged one are not indexed;
+    `raise_if_damaged()` raises the TFRecordError the Python reader would have
+    raised on reaching it."""
+
+    def __init__(self, path: str, verify: bool = True, parse: bool = True):
+        lib = _ffi.load()
+        self.path = path
+        size = os.path.getsize(path)
+        self._mm = None
+        if size:
+            with open(path, "rb") as fh:
+                self._mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+            self.buf = np.frombuffer(self._mm, np.uint8)
+        else:
+            self.buf = np.zeros(1, np.uint8)
+        base = self.buf.ctypes.data
+        n = ctypes.c_size_t(0)
+        rc = lib.jr_tfrecord_index(base, size, int(verify), None, None, 0, ctypes.byref(n))
+        self.error = None if rc == 0 else _ffi.last_error()
+        cnt = n.value
+        self.offsets = np.zeros(cnt, np.uint64)
+        self.lengths = np.zeros(cnt, np.uint64)
+        if cnt:
+            rc2 = lib.jr_tfrecord_index(base, size, int(verify), self.offsets.ctypes.data,
+                                        self.lengths.ctypes.data, cnt, ctypes.byref(n))
+            if rc2 != rc or n.value != cnt:       # the damage (if any) is where the count stopped
+                raise TFRecordError(f"{path}: changed while being indexed")
+        self.num_records = cnt
+        if parse:
+            self.enc_off = np.zeros(cnt, np.uint64)
+            self.enc_len = np.zeros(cnt, np.uint64)
+            self.label = np.zeros(cnt, np.int64)
+            self.height = np.zeros(cnt, np.int64)
+            self.width = np.zeros(cnt, np.int64)
+            self.status = np.zeros(cnt, np.int32)
+            _ffi.check("jr_example_parse_image", lib.jr_example_parse_image(
+                base, self.offsets.ctypes.data, self.lengths.ctypes.data, cnt, self.enc_off.ctypes.data,
+                self.enc_len.ctypes.data, self.label.ctypes.data, self.height.ctypes.data,
+                self.width.ctypes.data, self.status.ctypes.data))
+
+    def record(self, i: int) -> bytes:
+        o = int(self.offsets[i])
+        return self.buf[o:o + int(self.lengths[i])].tobytes()
+
+    def check(self, i: int) -> None:
+        st = int(self.status[i])
+        if st < 0:
+            raise ValueError(f"{self.path}: record {i} is not a serialized tf.train.Example")
+        if st:
+            key = _KEYS[(st & -st).bit_length() - 1]
+            raise ValueError(f"record is missing FixedLenFeature {key!r}")
+
+    def encoded(self, i: int) -> memoryview:
+        """The image/encoded bytes of record i (a view into the mapping)."""
+        o = int(self.enc_off[i])
+        return memoryview(self.buf[o:o + int(self.enc_len[i])])
+
+    def raise_if_damaged(self) -> None:
+        if self.error is not None:
+            raise TFRecordError(f"{self.path}: {self.error}")
 
 
 class TFRecordWriter:

@@ -30,6 +30,7 @@ as unpinned in DESIGN.md.
 """
 from __future__ import annotations
 
+import collections
 import io
 import os
 import queue
@@ -98,24 +99,22 @@ class Dataset:
         self._rng = np.random.default_rng(seed)
 
     # ------------------------------------------------------------- stages
-    def _records(self) -> Iterator[bytes]:
+    def _items(self) -> Iterator[Tuple["tfrecord.RecordFile", int]]:
+        """TFRecordDataset over the files in order: (file, record index) pairs.
+        Each file is mmap'd and indexed natively (jr_tfrecord_index) and its
+        Example features located in one call (jr_example_parse_image), so the
+        per-record host work is only the JPEG decode on the worker threads."""
         for path in self.files:
-            yield from tfrecord.read_records(path)
-
-    def _elements(self, pool: ThreadPoolExecutor) -> Iterator[Tuple[np.ndarray, np.ndarray]]:
-        """map(_parse_example, num_parallel_calls): output order = input order."""
-        window = []
-        depth = 4 * self.num_workers
-        for rec in self._records():
-            window.append(pool.submit(_parse_example, rec, self.image_dim, self.decode_dtype))
-            if len(window) >= depth:
-                yield window.pop(0).result()
-        for f in window:
-            yield f.result()
+            f = tfrecord.RecordFile(path)
+            for i in range(f.num_records):
+                yield f, i
+            f.raise_if_damaged()               # DataLossError where tf.data would raise it
 
     def _shuffled(self, it):
         """tf.data shuffle: fill a buffer, emit a uniformly random element and
-        refill its slot from the input; drain randomly at the end."""
+        refill its slot from the input; drain randomly at the end.  Applied to
+        (file, record) handles before the map: the map is elementwise, so the
+        emitted order is that of shuffling the decoded elements."""
         n = self.shuffle_buffer_size
         if n is None:
             yield from it
@@ -133,25 +132,73 @@ class Dataset:
             buf[i], buf[-1] = buf[-1], buf[i]
             yield buf.pop()
 
-    def _batches(self) -> Iterator[Tuple[np.ndarray, np.ndarray]]:
+    def _item_batches(self) -> Iterator[list]:
+        """repeat(num_epochs) then batch(batch_size), partial last batch kept."""
         epochs = self.num_epochs
+        e = 0
+        cur = []
+        while epochs is None or epochs < 0 or e < epochs:
+            any_elem = False
+            for it in self._shuffled(self._items()):
+                any_elem = True
+                cur.append(it)
+                if len(cur) == self.batch_size:
+                    yield cur
+                    cur = []
+            e += 1
+            if not any_elem:
+                break
+        if cur:
+            yield cur
+
+    def _decode_rows(self, items, rows, out) -> None:
+        """map(_parse_example) for rows [rows) of one batch, written in place."""
+        for r in rows:
+            f, i = items[r]
+            f.check(i)                                # FixedLenFeature checks (lib/dataset.py:12-16)
+            img = decode_jpeg(f.encoded(i))
+            if img.size != out[r].size:
+                raise ValueError(f"cannot reshape image of {img.size} values into {self.image_dim}")
+            img = img.reshape(self.image_dim)        # reshape, not transpose (App. C Q3)
+            if self.decode_dtype == "float32":
+                np.multiply(img, _SCALE, out=out[r])  # convert_image_dtype: f32(x) * f32(1/255)
+            else:
+                out[r] = img
+
+    def _submit(self, pool: ThreadPoolExecutor, items):
+        n = len(items)
+        out = np.empty([n] + self.image_dim, np.uint8 if self.decode_dtype == "uint8" else np.float32)
+        labels = np.array([f.label[i] for f, i in items], np.int64).astype(np.float32).reshape(n, 1)
+        chunk = max(1, -(-n // (2 * self.num_workers)))
+        futs = [pool.submit(self._decode_rows, items, range(a, min(n, a + chunk)), out)
+                for a in range(0, n, chunk)]
+        return out, labels, futs
+
+    def _batches(self) -> Iterator[Tuple[np.ndarray, np.ndarray]]:
+        depth = 2                                   # batches decoding ahead of the consumer
         with ThreadPoolExecutor(self.num_workers) as pool:
-            e = 0
-            imgs, labs = [], []
-            while epochs is None or epochs < 0 or e < epochs:   # repeat(num_epochs)
-                any_elem = False
-                for img, lab in self._shuffled(self._elements(pool)):
-                    any_elem = True
-                    imgs.append(img)
-                    labs.append(lab)
-                    if len(imgs) == self.batch_size:
-                        yield np.stack(imgs), np.stack(labs)
-                        imgs, labs = [], []
-                e += 1
-                if not any_elem:
-                    break
-            if imgs:                                          # partial last batch
-                yield np.stack(imgs), np.stack(labs)
+            inflight: "collections.deque" = collections.deque()
+            batches, err = self._item_batches(), None
+            try:
+                while True:
+                    try:
+                        items = next(batches)
+                    except StopIteration:
+                        break
+                    except Exception as e:              # damaged file: deliver what came before it
+                        err = e
+                        break
+                    inflight.append(self._submit(pool, items))
+                    if len(inflight) > depth:
+                        yield _collect(inflight.popleft())
+                while inflight:
+                    yield _collect(inflight.popleft())
+                if err is not None:
+                    raise err
+            finally:
+                for _, _, futs in inflight:
+                    for fu in futs:
+                        fu.cancel()
 
     def __iter__(self):
         gen = self._batches()
@@ -160,7 +207,19 @@ class Dataset:
         return _Prefetch(gen, max(1, int(self.prefetch_buffer_size) // self.batch_size + 1))
 
     def num_records(self) -> int:
-        return sum(1 for _ in self._records())
+        n = 0
+        for path in self.files:
+            f = tfrecord.RecordFile(path, parse=False)
+            f.raise_if_damaged()
+            n += f.num_records
+        return n
+
+
+def _collect(entry):
+    out, labels, futs = entry
+    for fu in futs:
+        fu.result()                                 # first failing row raises, in order
+    return out, labels
 
 
 class _Prefetch:

@@ -99,3 +99,140 @@ def test_repeat_epochs_and_channels_first_is_a_reshape(records):
     np.testing.assert_array_equal(cf.reshape(cl.shape), cl)       # App. C Q3: reshape, not transpose
     with pytest.raises(TypeError):
         D.initialize_dataset(records, 2, image_data_format="nchw")
+
+
+# ---- native record index / Example parse (jr_tfrecord_index, jr_example_parse_image)
+# checked against the pure-Python restatement of the same wire formats
+# (jr.tfrecord.read_records / decode_example) and the per-record element
+# function lib.dataset._parse_example.
+
+def _vint(v):
+    from jr import tfrecord
+    return tfrecord._varint(v)
+
+
+def _ex(entries):
+    """Example bytes from raw (name, Feature payload) map entries, in order."""
+    from jr import tfrecord as T
+    body = b"".join(T._field(1, 2, T._field(1, 2, n.encode()) + T._field(2, 2, f)) for n, f in entries)
+    return T._field(1, 2, body)
+
+
+def _bytes_feat(*vals):
+    from jr import tfrecord as T
+    return T._field(1, 2, b"".join(T._field(1, 2, v) for v in vals))
+
+
+def _int_feat(*vals, packed=True):
+    from jr import tfrecord as T
+    if packed:
+        return T._field(3, 2, T._field(1, 2, b"".join(_vint(v & (2 ** 64 - 1)) for v in vals)))
+    return T._field(3, 2, b"".join(bytes([1 << 3]) + _vint(v & (2 ** 64 - 1)) for v in vals))
+
+
+def _good(label=1, packed=True):
+    return [("image/encoded", _bytes_feat(b"\xff\xd8JPEGDATA")), ("image/format", _bytes_feat(b"jpeg")),
+            ("image/class/label", _int_feat(label, packed=packed)), ("image/height", _int_feat(299)),
+            ("image/width", _int_feat(299))]
+
+
+def test_native_index_matches_python_reader_and_stops_at_damage(tmp_path):
+    from jr import tfrecord
+    recs = [b"", b"a", b"x" * 100003] + [bytes([i]) * (i * 37) for i in range(40)]
+    path = str(tmp_path / "r.tfrecord")
+    with tfrecord.TFRecordWriter(path) as w:
+        for r in recs:
+            w.write(r)
+    f = tfrecord.RecordFile(path, parse=False)
+    assert f.error is None and f.num_records == len(recs)
+    assert [f.record(i) for i in range(f.num_records)] == list(tfrecord.read_records(path)) == recs
+    raw = bytearray(open(path, "rb").read())
+    bad_at = 12 + 0 + 4 + 12 + 1 + 4 + 12 + 50      # inside the third payload
+    raw[bad_at] ^= 0x40
+    open(path, "wb").write(bytes(raw))
+    f = tfrecord.RecordFile(path, parse=False)
+    assert f.num_records == 2 and "corrupted record data" in f.error
+    with pytest.raises(tfrecord.TFRecordError):
+        f.raise_if_damaged()
+    assert tfrecord.RecordFile(path, verify=False, parse=False).num_records == len(recs)
+    open(path, "wb").write(bytes(raw[:-3]))           # truncated tail
+    f = tfrecord.RecordFile(path, verify=False, parse=False)
+    assert f.num_records == len(recs) - 1 and "truncated" in f.error
+    empty = str(tmp_path / "e.tfrecord")
+    open(empty, "wb").close()
+    assert tfrecord.RecordFile(empty).num_records == 0
+
+
+def test_native_example_parse_matches_python_decoder(tmp_path):
+    from jr import tfrecord
+    cases = [
+        (_ex(_good(1)), 0),
+        (_ex(_good(0, packed=False)), 0),
+        (_ex(_good(-7)), 0),                                          # negative int64 label
+        (_ex(_good(1)[:2] + _good(1)[3:]), 4),                        # label missing
+        (_ex(_good(1)[:1] + [("image/format", _bytes_feat())] + _good(1)[2:]), 2),   # zero values
+        (_ex(_good(1)[:2] + [("image/class/label", _int_feat(0, 1))] + _good(1)[3:]), 4),  # two values
+        (_ex(_good(1)[:3] + [("image/height", _bytes_feat(b"299"))] + _good(1)[4:]), 8),  # wrong kind
+        (_ex(_good(1) + [("image/class/label", _int_feat(5))]), 0),  # duplicate key: last wins
+        (_ex([("extra", _int_feat(3, 4, 5))] + _good(1)), 0),        # unrelated features skipped
+        (b"\x0a\xff\xff", -1),                                        # truncated protobuf
+        (b"", 31),                                                    # empty Example: all missing
+    ]
+    path = str(tmp_path / "p.tfrecord")
+    with tfrecord.TFRecordWriter(path) as w:
+        for data, _ in cases:
+            w.write(data)
+    f = tfrecord.RecordFile(path)
+    assert list(f.status) == [st for _, st in cases]
+    for i, (data, st) in enumerate(cases):
+        if st == -1:
+            continue
+        ex = tfrecord.decode_example(data)
+        if st & 1 == 0:
+            assert bytes(f.encoded(i)) == ex["image/encoded"][0]
+        if st & 4 == 0:
+            assert int(f.label[i]) == ex["image/class/label"][0]
+        if st == 0:
+            assert int(f.height[i]) == ex["image/height"][0] == 299 and int(f.width[i]) == 299
+    with pytest.raises(ValueError, match="image/class/label"):
+        f.check(3)
+    with pytest.raises(ValueError, match="not a serialized"):
+        f.check(9)
+    assert int(f.label[7]) == 5
+
+
+def test_dataset_matches_per_record_python_path(records):
+    """Native-index pipeline (any worker count) == the per-record element
+    function over tfrecord.read_records, bit for bit, both decode dtypes."""
+    import lib.dataset as D
+    from jr import tfrecord
+    for dtype in ("float32", "uint8"):
+        want_x, want_y = [], []
+        for path in D._tfrecord_files_from_folder(records):
+            for rec in tfrecord.read_records(path):
+                x, y = D._parse_example(rec, [64, 64, 3], dtype)
+                want_x.append(x)
+                want_y.append(y)
+        for nw in (1, 3):
+            got = list(D.initialize_dataset(records, 5, image_dim=[64, 64], num_workers=nw, decode_dtype=dtype,
+                                            prefetch_buffer_size=10))
+            np.testing.assert_array_equal(np.concatenate([g[0] for g in got]), np.stack(want_x))
+            np.testing.assert_array_equal(np.concatenate([g[1] for g in got]), np.stack(want_y))
+
+
+def test_damaged_file_delivers_records_before_the_damage(tmp_path):
+    import lib.dataset as D
+    from jr import synth_records, tfrecord
+    d = str(tmp_path)
+    synth_records.write_split(d, 9, size=32, num_shards=1, name="train")
+    path = os.path.join(d, os.listdir(d)[0])
+    f = tfrecord.RecordFile(path)
+    raw = bytearray(open(path, "rb").read())
+    raw[int(f.offsets[6]) + 10] ^= 1                  # corrupt record 6
+    del f
+    open(path, "wb").write(bytes(raw))
+    got = []
+    with pytest.raises(tfrecord.TFRecordError):
+        for x, _ in D.initialize_dataset(d, 2, image_dim=[32, 32]):
+            got.append(len(x))
+    assert got == [2, 2, 2]                           # records 0-5, then DataLoss at record 6
