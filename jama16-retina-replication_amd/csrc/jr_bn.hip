@@ -22,9 +22,15 @@
 
 namespace jr {
 
-constexpr int kMaxChunks = 1024;  // partial sums per channel (finalize reads them)
+#ifndef JR_BN_MAX_CHUNKS
+#define JR_BN_MAX_CHUNKS 1024
+#endif
+#ifndef JR_BN_BWD_ROWS
+#define JR_BN_BWD_ROWS 8
+#endif
+constexpr int kMaxChunks = JR_BN_MAX_CHUNKS;  // partial sums per channel (finalize reads them)
 // rows in flight per thread in the reductions (16 B per row and operand)
-template <int MODE> constexpr int red_rows() { return MODE == 0 ? 16 : 8; }
+template <int MODE> constexpr int red_rows() { return MODE == 0 ? 16 : JR_BN_BWD_ROWS; }
 constexpr int kAppUnroll = 4;     // rows per thread in the elementwise passes
 
 // Same rounding in fwd and bwd so the ReLU mask is bit-identical.
