@@ -72,37 +72,66 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(jr_pool_desc d, const T* __
   }
 }
 
+// Backward as a gather over 2x2 input cells: input rows 2a, 2a+1 and columns
+// 2b, 2b+1 are covered only by the windows oh in {a-1, a}, ow in {b-1, b}, so
+// one thread loads those (at most) four windows' dy and argmax once and writes
+// the four input pixels of its cell -- one dy/argmax load per output pixel
+// instead of the 2.25 of a thread per input pixel.  Each input pixel still sums
+// its windows in (oh, ow) ascending order.
 template <typename T>
 __global__ void __launch_bounds__(256) k_maxpool_bwd(jr_pool_desc d, const uint8_t* __restrict__ argmax,
-                                                     const T* __restrict__ dy, T* dx, int accumulate) {
+                                                     const T* __restrict__ dy, T* __restrict__ dx, int accumulate) {
   const int c4 = d.c >> 2;
-  const int total = d.n * d.h * d.w * c4;
+  const int hc = (d.h + 1) >> 1, wc = (d.w + 1) >> 1;
+  const int total = d.n * hc * wc * c4;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int q = e % c4;
-    const int pix = e / c4;
-    const int iw = pix % d.w;
-    const int t = pix / d.w;
-    const int ih = t % d.h;
-    const int b = t / d.h;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    const int oh_lo = max(0, (ih - 1) / 2), oh_hi = min(d.ho - 1, ih / 2);
-    const int ow_lo = max(0, (iw - 1) / 2), ow_hi = min(d.wo - 1, iw / 2);
-    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const int pos = (ih - oh * 2) * 3 + (iw - ow * 2);
-        const int64_t op = ((int64_t)b * d.ho + oh) * d.wo + ow;
-        const uint32_t am = *reinterpret_cast<const uint32_t*>(argmax + op * d.c + q * 4);
-        const float4 g = P4<T>::ld(dy + op * d.y_c_stride + d.y_c_off + q * 4);
-        const float ga[4] = {g.x, g.y, g.z, g.w};
+    const int cell = e / c4;
+    const int cb = cell % wc;
+    const int t = cell / wc;
+    const int ca = t % hc;
+    const int b = t / hc;
+    uint32_t am[2][2];
+    float4 g[2][2];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if ((int)((am >> (8 * j)) & 0xff) == pos) acc[j] += ga[j];
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int oh = ca - 1 + i, ow = cb - 1 + j;
+        am[i][j] = 0xffffffffu;                  // position 255: matches no tap
+        g[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (oh >= 0 && oh < d.ho && ow >= 0 && ow < d.wo) {
+          const int64_t op = ((int64_t)b * d.ho + oh) * d.wo + ow;
+          am[i][j] = *reinterpret_cast<const uint32_t*>(argmax + op * d.c + q * 4);
+          g[i][j] = P4<T>::ld(dy + op * d.y_c_stride + d.y_c_off + q * 4);
+        }
       }
     }
-    T* p = dx + (int64_t)pix * d.x_c_stride + d.x_c_off + q * 4;
-    float4 o = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    if (accumulate) o = f4add(o, P4<T>::ld(p));
-    P4<T>::st(p, o);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const int ih = 2 * ca + u, iw = 2 * cb + v;
+        if (ih >= d.h || iw >= d.w) continue;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int r = u + 2 - 2 * i, c = v + 2 - 2 * j;   // tap of (ih, iw) in window (ca-1+i, cb-1+j)
+            if (r > 2 || c > 2) continue;                      // compile-time after unrolling
+            const float ga[4] = {g[i][j].x, g[i][j].y, g[i][j].z, g[i][j].w};
+#pragma unroll
+            for (int l = 0; l < 4; ++l)
+              if ((int)((am[i][j] >> (8 * l)) & 0xff) == r * 3 + c) acc[l] += ga[l];
+          }
+        }
+        T* p = dx + ((int64_t)(b * d.h + ih) * d.w + iw) * d.x_c_stride + d.x_c_off + q * 4;
+        float4 o = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        if (accumulate) o = f4add(o, P4<T>::ld(p));
+        P4<T>::st(p, o);
+      }
+    }
   }
 }
 
@@ -248,7 +277,7 @@ JR_API int jr_maxpool3x3s2_bwd(const jr_pool_desc* d, int dtype, const uint8_t* 
   int rc = check_pool(d, dtype, true);
   if (rc) return rc;
   if (!argmax || !dy || !dx) return fail(JR_ERR_INVALID, "maxpool_bwd: null pointer");
-  const int g = grid_for((int64_t)d->n * d->h * d->w * (d->c / 4));
+  const int g = grid_for((int64_t)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2) * (d->c / 4));
   if (dtype == JR_F32)
     hipLaunchKernelGGL(k_maxpool_bwd<float>, dim3(g), dim3(256), 0, as_stream(stream), *d, argmax,
                        (const float*)dy, (float*)dx, accumulate);
