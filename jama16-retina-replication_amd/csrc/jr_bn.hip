@@ -89,7 +89,10 @@ static ChunkGeom chunk_geom(int64_t m, int c, int vw) {
   // one unrolled batch of rows per thread at least; at most kMaxChunks chunks
   // (chunks of fewer rows -- more blocks for the 17x17 / 8x8 layers -- measured
   // slower: 1.47 -> 1.83 ms of reduce + 0.46 -> 0.65 ms of finalize per step)
-  const int un = red_rows<0>();
+#ifndef JR_BN_MIN_ROWS
+#define JR_BN_MIN_ROWS 16
+#endif
+  const int un = JR_BN_MIN_ROWS;
   int64_t rpc = std::max<int64_t>(ceil_div(m, kMaxChunks), (int64_t)rpp * un);
   rpc = ceil_div(rpc, (int64_t)rpp * un) * rpp * un;
   ChunkGeom g;
@@ -136,10 +139,20 @@ __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int 
       uint4 xr[U], gr[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        // rows past the chunk load the chunk's last row (always valid) and are
+        // zeroed after the load: zero bits = 0.0 in both dtypes, adds nothing.
+        // (A select between the loaded vector and a zero constant compiled to
+        // a FLAT load from a select of the row address and a scratch copy of
+        // the constant, with a scratch store per row.)
         const int64_t ri = r + (int64_t)u * rpp;
-        const uint4 z = make_uint4(0, 0, 0, 0);   // zero bits = 0.0 in both dtypes: adds nothing
-        xr[u] = ri < r1 ? *reinterpret_cast<const uint4*>(xp + ri * xs) : z;
-        if (MODE == 1) gr[u] = ri < r1 ? *reinterpret_cast<const uint4*>(gp + ri * dy_stride) : z;
+        const bool in = ri < r1;
+        const int64_t rc = in ? ri : r1 - 1;
+        const uint4 xv = *reinterpret_cast<const uint4*>(xp + rc * xs);
+        xr[u] = in ? xv : make_uint4(0, 0, 0, 0);
+        if (MODE == 1) {
+          const uint4 gv = *reinterpret_cast<const uint4*>(gp + rc * dy_stride);
+          gr[u] = in ? gv : make_uint4(0, 0, 0, 0);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
