@@ -31,7 +31,10 @@ namespace jr {
 constexpr int kMaxChunks = JR_BN_MAX_CHUNKS;  // partial sums per channel (finalize reads them)
 // rows in flight per thread in the reductions (16 B per row and operand)
 template <int MODE> constexpr int red_rows() { return MODE == 0 ? 16 : JR_BN_BWD_ROWS; }
-constexpr int kAppUnroll = 4;     // rows per thread in the elementwise passes
+#ifndef JR_BN_APP_UNROLL
+#define JR_BN_APP_UNROLL 4
+#endif
+constexpr int kAppUnroll = JR_BN_APP_UNROLL;  // rows per thread in the elementwise passes
 
 // Same rounding in fwd and bwd so the ReLU mask is bit-identical.
 __device__ __forceinline__ float bn_xhat(float x, float mean, float invstd) {

@@ -20,7 +20,7 @@ B = 64
 SHAPES = [(149, 32, 1), (147, 32, 1), (147, 64, 1), (73, 80, 1), (71, 192, 1),
           (35, 64, 12), (35, 48, 2), (35, 96, 9), (35, 32, 1), (17, 384, 1), (17, 192, 18), (17, 128, 6),
           (17, 160, 12), (8, 320, 3), (8, 192, 3), (8, 384, 8), (8, 448, 2), (17, 96, 1)]
-tot = 0.0
+tot = tot_apply = 0.0
 for h, c, cnt in SHAPES:
     m = B * h * h
     x = torch.randn(m * c, device="cuda").to(TD)
@@ -48,6 +48,20 @@ for h, c, cnt in SHAPES:
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / n
     gbs = 3 * m * c * x.element_size() / us / 1e3     # algorithmic: read x, dy once; write dx
+
+    def fwd():
+        _ffi.check("jr_bn_relu_apply", L.jr_bn_relu_apply(DT, P(x), 0, c, m, c, P(mean), P(invstd), P(beta),
+                                                          P(dx), 0, c, None))
+    for _ in range(5):
+        fwd()
+    e0.record()
+    for _ in range(n):
+        fwd()
+    e1.record()
+    torch.cuda.synchronize()
+    ua = e0.elapsed_time(e1) * 1e3 / n
     tot += us * cnt
-    print(f"{h:4d}^2 x {c:4d}  x{cnt:2d}: {us:8.1f} us  {gbs:7.0f} GB/s (3 passes)")
-print(f"weighted total {tot:.1f} us  [{os.path.basename(_ffi.LIB_PATH)}]")
+    tot_apply += ua * cnt
+    print(f"{h:4d}^2 x {c:4d}  x{cnt:2d}: bwd {us:8.1f} us  {gbs:7.0f} GB/s (3 passes) | apply {ua:7.1f} us "
+          f"{2 * m * c * x.element_size() / ua / 1e3:7.0f} GB/s")
+print(f"weighted total bwd {tot:.1f} us, apply {tot_apply:.1f} us  [{os.path.basename(_ffi.LIB_PATH)}]")
