@@ -329,6 +329,60 @@ def test_avgpool(shape):
     assert relerr(host(DX).reshape(shape), dx_ref) < 1e-6
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("shape", [(2, 147, 147, 64), (2, 17, 17, 48), (1, 10, 9, 8), (1, 3, 3, 4)])
+def test_pools_in_channel_slices(shape, dtype):
+    """Pools reading and writing channel slices of wider NHWC buffers (the
+    concat-free block layout), both dtypes, accumulate and overwrite: the
+    2x2-cell max-pool backward and the sliding-box avg-pool against the oracle
+    on the same (bf16-rounded) inputs; bytes outside the slices untouched."""
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, c = shape
+    td = torch.bfloat16 if dtype == "bf16" else torch.float32
+    dt = 1 if dtype == "bf16" else 0
+    tol = 2.0 ** -7 if dtype == "bf16" else 1e-6
+    rng = np.random.default_rng(sum(shape) + 7)
+    rnd = lambda a: torch.as_tensor(a).to(td).float().numpy().astype(np.float64)  # noqa: E731
+    xo, xs, yo, ys = 4, c + 12, 8, c + 16
+    x = rnd(np.maximum(rng.standard_normal(shape), 0))
+    xbuf = np.full((n, h, w, xs), 3.0)
+    xbuf[..., xo:xo + c] = x
+    X = dev(xbuf, td)
+    y_ref, am_ref = R.maxpool3x3s2(x)
+    ho, wo = y_ref.shape[1:3]
+    d = ffi.PoolDesc(n, h, w, c, ho, wo, xo, xs, yo, ys)
+    Y = torch.full((n * ho * wo * ys,), 5.0, device="cuda", dtype=td)
+    AM = torch.zeros(n * ho * wo * c, dtype=torch.uint8, device="cuda")
+    ffi.check("mp fwd", L.jr_maxpool3x3s2_fwd(ctypes.byref(d), dt, X.data_ptr(), Y.data_ptr(), AM.data_ptr(), None))
+    yg = host(Y.float()).reshape(n, ho, wo, ys)
+    assert np.array_equal(yg[..., yo:yo + c], y_ref) and np.all(yg[..., :yo] == 5) and np.all(yg[..., yo + c:] == 5)
+    assert np.array_equal(host(AM).reshape(n, ho, wo, c), am_ref)
+    dy = rnd(rng.standard_normal(y_ref.shape))
+    dybuf = np.zeros((n, ho, wo, ys))
+    dybuf[..., yo:yo + c] = dy
+    dx_ref = R.maxpool3x3s2_bwd(dy, am_ref, x.shape)
+    for acc in (0, 1):
+        DX = dev(np.full((n, h, w, xs), 2.0), td)
+        ffi.check("mp bwd", L.jr_maxpool3x3s2_bwd(ctypes.byref(d), dt, AM.data_ptr(), dev(dybuf, td).data_ptr(),
+                                                  DX.data_ptr(), acc, None))
+        g = host(DX.float()).reshape(n, h, w, xs)
+        assert np.all(g[..., :xo] == 2) and np.all(g[..., xo + c:] == 2)
+        assert relerr(g[..., xo:xo + c], dx_ref + 2.0 * acc) <= tol
+    da = ffi.PoolDesc(n, h, w, c, h, w, xo, xs, yo, ys)
+    Ya = torch.full((n * h * w * ys,), 5.0, device="cuda", dtype=td)
+    ffi.check("ap fwd", L.jr_avgpool3x3s1_fwd(ctypes.byref(da), dt, X.data_ptr(), Ya.data_ptr(), None))
+    ya = host(Ya.float()).reshape(n, h, w, ys)
+    assert relerr(ya[..., yo:yo + c], R.avgpool3x3s1_same(x)) <= tol and np.all(ya[..., :yo] == 5)
+    dya = np.zeros((n, h, w, ys))
+    dya[..., yo:yo + c] = rnd(rng.standard_normal((n, h, w, c)))
+    DXa = dev(np.full((n, h, w, xs), 2.0), td)
+    ffi.check("ap bwd", L.jr_avgpool3x3s1_bwd(ctypes.byref(da), dt, dev(dya, td).data_ptr(), DXa.data_ptr(), 1, None))
+    ga = host(DXa.float()).reshape(n, h, w, xs)
+    assert relerr(ga[..., xo:xo + c], R.avgpool3x3s1_same_bwd(dya[..., yo:yo + c]) + 2.0) <= tol
+    assert np.all(ga[..., :xo] == 2) and np.all(ga[..., xo + c:] == 2)
+
+
 def test_gap_head_loss():
     ffi = _lib()
     L = ffi.load()
