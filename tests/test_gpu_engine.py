@@ -235,3 +235,41 @@ def test_lanes_are_bitwise_single_stream(dtype):
     for e in (many, graph, graph2):
         assert np.array_equal(one.params_numpy(), e.params_numpy())
         assert one.loss_value() == e.loss_value()
+
+
+def test_ensemble_auc_matches_oracle():
+    """evaluate.py's ensemble (evaluate.py:214-217 + lib/evaluation.py): M
+    members' sigmoid predictions over the test batches (batch statistics per
+    eval batch, App. C Q1), linear mean, TF 200-threshold AUC.  GPU vs the
+    fp64 oracle on the same weights and batches: predictions within 1e-4,
+    ensemble AUC equal to 3 decimals (north_star), Brier within 1e-5."""
+    from jr.engine import Engine
+    from jr import synth
+    from oracle.inception_ref import InceptionV3Ref
+    from oracle import metrics_ref as M
+    res, B, nb, members = 107, 8, 3, 2
+    imgs = synth.fundus_batch(300, B * nb, res)
+    y = synth.labels(300, B * nb, p=0.4)
+    gpu, ref = [], []
+    for m in range(members):
+        eng = Engine(B, res, res, seed=m, train=False)
+        oracle = InceptionV3Ref(_oracle_params(eng), torch.float64, requires_grad=False)
+        pg, pr = [], []
+        for b in range(nb):
+            x = imgs[b * B:(b + 1) * B]
+            eng.set_batch(x)
+            eng.forward()
+            pg.append(eng.predictions().ravel())
+            with torch.no_grad():
+                _, p, _ = oracle.forward(x.astype(np.float32) * np.float32(1 / 255))
+            pr.append(p.numpy().ravel())
+        gpu.append(np.concatenate(pg))
+        ref.append(np.concatenate(pr))
+        del eng
+    gpu, ref = np.stack(gpu), np.stack(ref)
+    assert np.max(np.abs(gpu - ref)) < 1e-4
+    ens_g, ens_r = gpu.mean(axis=0), ref.mean(axis=0)
+    yy = y.ravel()
+    auc_g, auc_r = M.auc(yy, ens_g), M.auc(yy, ens_r)
+    assert abs(auc_g - auc_r) < 5e-4, (auc_g, auc_r)
+    assert abs(M.brier(yy, ens_g) - M.brier(yy, ens_r)) < 1e-5
