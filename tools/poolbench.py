@@ -19,7 +19,7 @@ MAXP = [(147, 64), (71, 192), (35, 288), (17, 768)]
 AVGP = [(35, 192), (35, 256), (35, 288), (17, 768), (17, 768), (17, 768), (17, 768), (8, 1280), (8, 2048)]
 
 
-def timeit(fn, n=50):
+def timeit(fn, n=int(os.environ.get("POOLBENCH_N", "50"))):
     for _ in range(5):
         fn()
     torch.cuda.synchronize()
