@@ -141,7 +141,10 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(jr_pool_desc d, const uint8
 // instead of 9 times (a thread per output was L2-bound; this is +1.2 % per
 // training step).  The backward is the same box over z = dy / count
 // (count = ch(oh) * cw(ow), the in-bounds taps of the output window).
-constexpr int kStrip = 8;
+#ifndef JR_POOL_STRIP
+#define JR_POOL_STRIP 8
+#endif
+constexpr int kStrip = JR_POOL_STRIP;
 
 template <typename T, bool BWD>
 __device__ __forceinline__ float4 box_row(const jr_pool_desc& d, const T* __restrict__ src, int b, int h, int w,
