@@ -32,6 +32,16 @@
  *    fp32 rounding and the result differs from JR_F32 only in summation
  *    order (bf16x9-style fp32 emulation).  Non-finite inputs give NaN where
  *    JR_F32 could give +-inf.
+ *    JR_F32_X8P (convolution entry points only) = the JR_F32_X8 arithmetic
+ *    with the split done once, outside the GEMM: every operand arrives as its
+ *    three bf16 planes h, m, l (x = h + m + l exactly; jr_split_x8p,
+ *    jr_conv_weights_x8p*), stored back to back, each plane in the JR_BF16
+ *    layout of that operand (channel radices padded to 8; fwd filter
+ *    W^T [c_out][kh][kw][c8], bwd_data filter HWIO).  The plane stride is the
+ *    plane's element count as the descriptor implies: n*h*w*x_c_stride (x),
+ *    n*ho*wo*y_c_stride (dy), c_out*kh*kw*c8 (W^T), kh*kw*c_in*c_out (HWIO).
+ *    Eight MFMAs per product in the JR_F32_X8 order; outputs (y, dx, dw) are
+ *    fp32 exactly as for JR_F32.
  */
 #ifndef JR_H_
 #define JR_H_
@@ -51,7 +61,7 @@ typedef enum jr_status {
   JR_ERR_WORKSPACE = -4    /* workspace smaller than *_workspace_size      */
 } jr_status;
 
-typedef enum jr_dtype { JR_F32 = 0, JR_BF16 = 1, JR_F32_X8 = 2 } jr_dtype;
+typedef enum jr_dtype { JR_F32 = 0, JR_BF16 = 1, JR_F32_X8 = 2, JR_F32_X8P = 3 } jr_dtype;
 
 typedef enum jr_conv_op { JR_CONV_FWD = 0, JR_CONV_BWD_DATA = 1, JR_CONV_BWD_FILTER = 2 } jr_conv_op;
 
@@ -210,6 +220,22 @@ int jr_conv_weights_bf16(const float* w, int32_t kh, int32_t kw, int32_t c_in, i
                          void* w_t, void* stream);
 int jr_conv_weights_bf16_multi(const jr_wprep* layers, int32_t n_layers, int32_t total_tiles, const float* src,
                                void* hwio, void* wt, void* stream);
+/* JR_F32_X8P filter operands: the same two layouts as three bf16 planes
+ * each (h, m, l of the exact split), plane stride = the layer's element
+ * count (kh*kw*c_in*c_out for HWIO, c_out*kh*kw*c8 for W^T); in the _multi
+ * form hwio_off / wt_off address each layer's first plane. */
+int jr_conv_weights_x8p(const float* w, int32_t kh, int32_t kw, int32_t c_in, int32_t c_out, void* w_hwio,
+                        void* w_t, void* stream);
+int jr_conv_weights_x8p_multi(const jr_wprep* layers, int32_t n_layers, int32_t total_tiles, const float* src,
+                              void* hwio, void* wt, void* stream);
+/* Exact three-way bf16 split of an fp32 activation / gradient slice for
+ * JR_F32_X8P: h = bf16_rn(x), m = bf16_rn(x - h), l = x - h - m (exact in
+ * bf16).  src [rows][src_stride] channels [src_off, src_off + c) ->
+ * dst + p * plane_stride (p = 0, 1, 2 for h, m, l), each [rows][dst_stride],
+ * channels [dst_off, dst_off + c_pad); channels c..c_pad-1 are written as
+ * zeros (the conv1 image: c = 3, c_pad = 8). */
+int jr_split_x8p(const float* src, int64_t rows, int32_t c, int32_t src_off, int32_t src_stride, void* dst,
+                 int32_t c_pad, int32_t dst_off, int32_t dst_stride, int64_t plane_stride, void* stream);
 
 /* ---- dtype helpers --------------------------------------------------- */
 int jr_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream);

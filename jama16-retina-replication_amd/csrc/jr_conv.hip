@@ -612,12 +612,17 @@ struct Plan {
 
 // Channel padding of the reduction operand: 16 B DMA pieces hold 4 fp32 or
 // 8 bf16 channels.
+static bool bf16_operands(int dtype) { return dtype == JR_BF16 || dtype == JR_F32_X8P; }
 static int chan_pad(int c, int dtype) {
-  const int q = dtype == JR_BF16 ? 8 : 4;
+  const int q = bf16_operands(dtype) ? 8 : 4;
   return (c + q - 1) / q * q;
 }
-static const TileCfg* cfg_table(int dtype) { return dtype == JR_BF16 ? kCfgsBf16 : kCfgs; }
-static int cfg_count(int dtype) { return dtype == JR_BF16 ? kNumCfgsBf16 : kNumCfgs; }
+static const TileCfg* cfg_table(int dtype) {
+  return dtype == JR_BF16 ? kCfgsBf16 : dtype == JR_F32_X8P ? kCfgsX8P : kCfgs;
+}
+static int cfg_count(int dtype) {
+  return dtype == JR_BF16 ? kNumCfgsBf16 : dtype == JR_F32_X8P ? kNumCfgsX8P : kNumCfgs;
+}
 
 static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
   int k = 0;
@@ -767,8 +772,9 @@ static void launch_op(int cfg, const ConvArgs& a, dim3 grid, hipStream_t s) {
 }
 
 static int validate(const jr_conv_desc* d, int op, int dtype) {
-  if (dtype != JR_F32 && dtype != JR_BF16 && dtype != JR_F32_X8) return fail(JR_ERR_INVALID, "conv: bad dtype");
-  const int q = dtype == JR_BF16 ? 8 : 4;   // channels per 16 B piece
+  if (dtype != JR_F32 && dtype != JR_BF16 && dtype != JR_F32_X8 && dtype != JR_F32_X8P)
+    return fail(JR_ERR_INVALID, "conv: bad dtype");
+  const int q = bf16_operands(dtype) ? 8 : 4;   // channels per 16 B piece
   if (!d) return fail(JR_ERR_INVALID, "conv: null descriptor");
   if (op < OP_FWD || op > OP_WGRAD) return fail(JR_ERR_INVALID, "conv: bad op");
   if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->c_in <= 0 || d->c_out <= 0 || d->kh <= 0 ||
@@ -832,10 +838,10 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     a.C = static_cast<float*>(out);
   }
   dim3 grid(p.mt * p.nt, 1, p.splits);
-  if (dtype == JR_BF16) {
-    const TileCfg& t = kCfgsBf16[p.tile];
+  if (bf16_operands(dtype)) {
+    const TileCfg& t = cfg_table(dtype)[p.tile];
     const bool fast = OP == OP_WGRAD ? a.wo >= t.bk : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
-    launch_conv_bf16(OP, p.tile, fast, a, grid, s);
+    launch_conv_bf16(OP, p.tile, fast, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
   } else if (dtype == JR_F32_X8) {
     launch_op<OP, 0, true>(p.tile, a, grid, s);
   } else {
@@ -936,6 +942,15 @@ static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, con
   a.A = static_cast<const float*>(A);   // bf16 kernels reinterpret
   a.B = static_cast<const float*>(B);
   a.accumulate = accumulate;
+  if (dtype == JR_F32_X8P) {   // plane strides = each operand tensor's element count (jr.h)
+    const long long xe = (long long)d->n * d->h * d->w * d->x_c_stride;
+    const long long ye = (long long)d->n * d->ho * d->wo * d->y_c_stride;
+    const long long we = (long long)d->kh * d->kw * d->c_in * d->c_out;                  // HWIO
+    const long long wt = (long long)d->c_out * d->kh * d->kw * chan_pad(d->c_in, dtype);  // W^T
+    if (op == OP_FWD) { a.a_ps = xe; a.b_ps = wt; }
+    else if (op == OP_DGRAD) { a.a_ps = ye; a.b_ps = we; }
+    else { a.a_ps = xe; a.b_ps = ye; }
+  }
   hipStream_t s = as_stream(stream);
   void* out = C;
   if (op == OP_FWD) {
@@ -1135,7 +1150,7 @@ JR_API int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const vo
 }
 
 JR_API int jr_conv2d_num_configs(int dtype) {
-  return dtype == JR_BF16 || dtype == JR_F32 || dtype == JR_F32_X8 ? cfg_count(dtype) : 0;
+  return dtype == JR_BF16 || dtype == JR_F32 || dtype == JR_F32_X8 || dtype == JR_F32_X8P ? cfg_count(dtype) : 0;
 }
 
 // Diagnostic: time `reps` launches of one FWD GEMM (no split-K) of tile

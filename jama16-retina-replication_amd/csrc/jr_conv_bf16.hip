@@ -15,6 +15,15 @@
 //     two reads give a lane its 8 k values.
 // Outputs: FWD / DGRAD write bf16 (fp32 accumulate, one rounding; split-K
 // slabs stay fp32 and the reduce rounds), WGRAD writes fp32 dW.
+//
+// NP = 3 is JR_F32_X8P: fp32 arithmetic from operands that arrive already
+// split into three bf16 planes (x = h + m + l exactly, jr_split_x8p /
+// jr_conv_weights_x8p_multi).  Every DMA piece is issued once per plane
+// (the same source offset in each plane, plane strides g.a_ps / g.b_ps),
+// each fragment is read once per plane, and eight MFMAs per (i, j, k-step)
+// accumulate hh mh hm mm lh hl ml lm (A plane x B plane) in fp32 — the
+// products and per-accumulator order of the JR_F32_X8 kernel (jr_conv.hip),
+// without its in-register split VALU.  Outputs are fp32 as for JR_F32.
 #include "jr_conv_impl.h"
 
 namespace jr {
@@ -30,8 +39,9 @@ __device__ __forceinline__ s16x4 lds_tr(const uint16_t* p) {
       (__attribute__((address_space(3))) s16x4*)(const_cast<uint16_t*>(p)));
 }
 
-template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT>
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, int NP>
 __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
+  static_assert(NP == 1 || NP == 3, "one bf16 plane, or the h / m / l planes of X8P");
   constexpr int WGN = 4 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
@@ -46,7 +56,8 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   constexpr int A_PW = (A_INSTR + 3) / 4, B_PW = (B_INSTR + 3) / 4;  // per wave
   static_assert(ASZ % 512 == 0 && BSZ % 512 == 0, "tile must be whole DMA instructions");
   static_assert(BK % 16 == 0 && QPR <= 8, "BK must be 16..64");
-  constexpr int SMEM = NBUF * (ASZ + BSZ) > 8 * stage_floats<WN>() ? NBUF * (ASZ + BSZ) : 8 * stage_floats<WN>();
+  constexpr int STAGE = NP * (ASZ + BSZ);    // one ring slot: NP A planes, then NP B planes
+  constexpr int SMEM = NBUF * STAGE > 8 * stage_floats<WN>() ? NBUF * STAGE : 8 * stage_floats<WN>();
   __shared__ __attribute__((aligned(1024))) uint16_t smem[SMEM];
 
   const uint16_t* __restrict__ gA = reinterpret_cast<const uint16_t*>(g.A);
@@ -64,6 +75,7 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   const int kt1 = min(g.ktiles, kt0 + g.kt_per_split);
   const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
   const int cred = OP == OP_FWD ? g.cp : g.cout;
+  const long long psA = NP > 1 ? g.a_ps : 0, psB = NP > 1 ? g.b_ps : 0;
   // FWD/DGRAD: UT = wave-uniform tap (cred % BK == 0); WGRAD: UT = wo >= BK.
   constexpr bool ut = UT && OP != OP_WGRAD;
 
@@ -186,6 +198,11 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   const bool a_multi = !MC ? (cred < BK) : (!UT && g.wo < BK);
   const bool b_multi = (OP == OP_DGRAD) ? (g.cout < BK) : false;
 
+  // One piece into every plane image (out-of-bounds: the zero page, all planes).
+  auto put = [&](bool ok, const uint16_t* src, uint16_t* dst, long long ps, int isz) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) dma16(ok ? src + p * ps : zp, dst + p * isz);
+  };
   // DMA of one operand piece of tile kt (d < A_PW: A slot d, else B slot).
   auto issue_piece = [&](int kt, int d, uint16_t* __restrict__ As, uint16_t* __restrict__ Bs) {
     if (d < A_PW) {
@@ -204,29 +221,27 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
         }
         const int hmax = OP == OP_FWD ? g.h : g.ho, wmax = OP == OP_FWD ? g.w : g.wo;
         const bool ok = (unsigned)(a_p0[i] + dr) < (unsigned)hmax && (unsigned)(a_p1[i] + dc) < (unsigned)wmax;
-        dma16(ok ? a_ptr[i] + off : zp, As + j * 512);
+        put(ok, a_ptr[i] + off, As + j * 512, psA, ASZ);
       } else {
-        const uint16_t* src = zp;
+        bool ok;
+        const uint16_t* p;
         if constexpr (OP == OP_FWD) {
           const int hi = a_p0[i] + a_s0[i], wi = a_p1[i] + a_s1[i];
-          const bool ok = (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w && a_s0[i] < g.kh;
-          const uint16_t* p = gA + ((a_p2[i] + hi * g.w + wi) * g.xs + g.xo + a_s2[i]);
-          src = ok ? p : zp;
+          ok = (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w && a_s0[i] < g.kh;
+          p = gA + ((a_p2[i] + hi * g.w + wi) * g.xs + g.xo + a_s2[i]);
           adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cp, g.kw, a_multi);
         } else if constexpr (OP == OP_DGRAD) {
           const int oh = a_p0[i] - a_s0[i], ow = a_p1[i] - a_s1[i];
-          const bool ok = (unsigned)oh < (unsigned)g.ho && (unsigned)ow < (unsigned)g.wo && a_s0[i] < g.na;
-          const uint16_t* p = gA + ((a_p2[i] + oh * g.wo + ow) * g.ys + g.yo + a_s2[i]);
-          src = ok ? p : zp;
+          ok = (unsigned)oh < (unsigned)g.ho && (unsigned)ow < (unsigned)g.wo && a_s0[i] < g.na;
+          p = gA + ((a_p2[i] + oh * g.wo + ow) * g.ys + g.yo + a_s2[i]);
           adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cout, g.nb, a_multi);
         } else {  // WGRAD
           const int hi = a_s1[i] * g.sh + a_p0[i], wi = a_s2[i] * g.sw + a_p1[i];
-          const bool ok = a_s0[i] < g.n && (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w;
-          const uint16_t* p = gA + (((a_s0[i] * g.h + hi) * g.w + wi) * g.xs + g.xo + a_p2[i]);
-          src = ok ? p : zp;
+          ok = a_s0[i] < g.n && (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w;
+          p = gA + (((a_s0[i] * g.h + hi) * g.w + wi) * g.xs + g.xo + a_p2[i]);
           adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.wo, g.ho, a_multi);
         }
-        dma16(src, As + j * 512);
+        put(ok, p, As + j * 512, psA, ASZ);
       }
       return;
     }
@@ -236,22 +251,22 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
     if constexpr (OP == OP_FWD) {
       const int k = b_s0[i] + (kt - kt0) * BK;
       const bool ok = b_p0[i] >= 0 && k < g.K;
-      dma16(ok ? b_ptr[i] + (kt - kt0) * BK : zp, Bs + j * 512);
+      put(ok, b_ptr[i] + (kt - kt0) * BK, Bs + j * 512, psB, BSZ);
     } else if constexpr (OP == OP_DGRAD) {
       if constexpr (ut) {
         const long long off = (long long)((g.r0 + g.sh * t_r) * g.kw + (g.c0 + g.sw * t_c)) * g.cin * g.cout + t_ch;
-        dma16(b_p0[i] >= 0 ? b_ptr[i] + off : zp, Bs + j * 512);
+        put(b_p0[i] >= 0, b_ptr[i] + off, Bs + j * 512, psB, BSZ);
       } else {
         const bool ok = b_p0[i] >= 0 && b_s0[i] < g.na;
         const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
         const uint16_t* p = gB + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
-        dma16(ok ? p : zp, Bs + j * 512);
+        put(ok, p, Bs + j * 512, psB, BSZ);
         adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
       }
     } else {  // WGRAD
       const int k = b_s0[i] + (kt - kt0) * BK;
       const bool ok = b_p0[i] >= 0 && k < g.K;
-      dma16(ok ? b_ptr[i] + (long long)(kt - kt0) * BK * g.ys : zp, Bs + j * 512);
+      put(ok, b_ptr[i] + (long long)(kt - kt0) * BK * g.ys, Bs + j * 512, psB, BSZ);
     }
   };
   auto advance = [&]() {
@@ -283,12 +298,14 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   const int l31 = lane & 31, lh = lane >> 5;
   // transposed-read lane roles (MC): 16-lane group g16 = lh*2 + hb
   const int hb = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
-  constexpr int per_tile = A_INSTR / 4 + B_INSTR / 4;
+  constexpr int per_tile = NP * (A_INSTR / 4 + B_INSTR / 4);   // DMA instructions per wave and tile (min)
 
   auto step = [&](int kt, auto do_issue, const uint16_t* __restrict__ As, const uint16_t* __restrict__ Bs,
                   uint16_t* __restrict__ wA, uint16_t* __restrict__ wB) {
     constexpr bool DO_ISSUE = decltype(do_issue)::value;
-    bf16x8 af[TM][KSTEPS], bfr[TN][KSTEPS];
+    bf16x8 af[NP][TM][KSTEPS], bfr[NP][TN][KSTEPS];
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) {
 #pragma unroll
@@ -296,11 +313,11 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
         if constexpr (!MC) {
           const int row = wm0 + i * 32 + l31;
           const int f = (row / SWZ) % QPR;
-          af[i][s] = *reinterpret_cast<const bf16x8*>(As + row * BK + (((2 * s + lh) ^ f) * 8));
+          af[p][i][s] = *reinterpret_cast<const bf16x8*>(As + p * ASZ + row * BK + (((2 * s + lh) ^ f) * 8));
         } else {
-          const uint16_t* p = As + (16 * s + 8 * lh + tq) * BM + wm0 + i * 32 + 16 * hb + 4 * tp;
-          const s16x4 lo = lds_tr(p), hi = lds_tr(p + 4 * BM);
-          af[i][s] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          const uint16_t* q = As + p * ASZ + (16 * s + 8 * lh + tq) * BM + wm0 + i * 32 + 16 * hb + 4 * tp;
+          const s16x4 lo = lds_tr(q), hi = lds_tr(q + 4 * BM);
+          af[p][i][s] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
       }
 #pragma unroll
@@ -308,13 +325,37 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
         if constexpr (!MC) {
           const int row = wn0 + j * 32 + l31;
           const int f = (row / SWZ) % QPR;
-          bfr[j][s] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + (((2 * s + lh) ^ f) * 8));
+          bfr[p][j][s] = *reinterpret_cast<const bf16x8*>(Bs + p * BSZ + row * BK + (((2 * s + lh) ^ f) * 8));
         } else {
-          const uint16_t* p = Bs + (16 * s + 8 * lh + tq) * BN + wn0 + j * 32 + 16 * hb + 4 * tp;
-          const s16x4 lo = lds_tr(p), hi = lds_tr(p + 4 * BN);
-          bfr[j][s] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          const uint16_t* q = Bs + p * BSZ + (16 * s + 8 * lh + tq) * BN + wn0 + j * 32 + 16 * hb + 4 * tp;
+          const s16x4 lo = lds_tr(q), hi = lds_tr(q + 4 * BN);
+          bfr[p][j][s] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
       }
+    }
+    if constexpr (NP == 3) {
+      // eight products per k-step, (A plane, B plane) in the JR_F32_X8 order
+      // hh mh hm mm lh hl ml lm; the DMA pieces of tile kt+NBUF-1 are spread
+      // over the product groups (each piece = one DMA per plane)
+      constexpr int PA[8] = {0, 1, 0, 1, 2, 0, 1, 2}, PB[8] = {0, 0, 1, 1, 0, 2, 2, 1};
+      constexpr int NG = 8 * KSTEPS;
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[PA[t]][i][s], bfr[PB[t]][j][s], acc[i][j], 0, 0, 0);
+          if constexpr (DO_ISSUE) {
+            const int gi = s * 8 + t;
+#pragma unroll
+            for (int d = gi * NPIECE / NG; d < (gi + 1) * NPIECE / NG; ++d) issue_piece(kt + NBUF - 1, d, wA, wB);
+          }
+        }
+      if constexpr (DO_ISSUE) advance();
+      return;
     }
     // MFMAs of k-step s, then this step's share of the DMA pieces of tile
     // kt+NBUF-1 (the LDS-DMA intrinsic is a scheduling boundary for hipcc)
@@ -324,7 +365,7 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i][s], bfr[0][j][s], acc[i][j], 0, 0, 0);
       if constexpr (DO_ISSUE) {
 #pragma unroll
         for (int d = s * NPIECE / KSTEPS; d < (s + 1) * NPIECE / KSTEPS; ++d) issue_piece(kt + NBUF - 1, d, wA, wB);
@@ -332,8 +373,8 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
     }
     if constexpr (DO_ISSUE) advance();
   };
-  auto buf_a = [&](int b) { return smem + b * (ASZ + BSZ); };
-  auto buf_b = [&](int b) { return smem + b * (ASZ + BSZ) + ASZ; };
+  auto buf_a = [&](int b) { return smem + b * STAGE; };
+  auto buf_b = [&](int b) { return smem + b * STAGE + NP * ASZ; };
 
   if (kt0 < kt1) {
 #pragma unroll
@@ -363,38 +404,46 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   }
 
   // ---------------------------------------------------------------- epilogue
-  conv_epilogue<OP, WM, TM, TN, true>(g, acc, reinterpret_cast<float*>(smem) + wave * stage_floats<WN>(), m0 + wm0,
+  conv_epilogue<OP, WM, TM, TN, NP == 1>(g, acc, reinterpret_cast<float*>(smem) + wave * stage_floats<WN>(), m0 + wm0,
                                       n0 + wn0, lane);
 }
 
-template <int OP, int C>
+template <int OP, int C, int NP>
 static void launch_tile(bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  constexpr TileCfg t = kCfgsBf16[C];
+  constexpr TileCfg t = NP == 1 ? kCfgsBf16[C] : kCfgsX8P[C];
   if (fast)
-    hipLaunchKernelGGL((k_conv_bf16<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv_bf16<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, NP>), grid, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((k_conv_bf16<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv_bf16<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, NP>), grid, dim3(256), 0, s, a);
 }
 
-template <int OP>
+template <int OP, int NP>
 static void launch_op_bf16(int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  static_assert(kNumCfgsBf16 == 8, "keep the switch in sync with kCfgsBf16");
+  static_assert(kNumCfgsBf16 == 10 && kNumCfgsX8P == 10, "keep the switch in sync with kCfgsBf16 / kCfgsX8P");
   switch (tile) {
-    case 0: launch_tile<OP, 0>(fast, a, grid, s); break;
-    case 1: launch_tile<OP, 1>(fast, a, grid, s); break;
-    case 2: launch_tile<OP, 2>(fast, a, grid, s); break;
-    case 3: launch_tile<OP, 3>(fast, a, grid, s); break;
-    case 4: launch_tile<OP, 4>(fast, a, grid, s); break;
-    case 5: launch_tile<OP, 5>(fast, a, grid, s); break;
-    case 6: launch_tile<OP, 6>(fast, a, grid, s); break;
-    default: launch_tile<OP, 7>(fast, a, grid, s); break;
+    case 0: launch_tile<OP, 0, NP>(fast, a, grid, s); break;
+    case 1: launch_tile<OP, 1, NP>(fast, a, grid, s); break;
+    case 2: launch_tile<OP, 2, NP>(fast, a, grid, s); break;
+    case 3: launch_tile<OP, 3, NP>(fast, a, grid, s); break;
+    case 4: launch_tile<OP, 4, NP>(fast, a, grid, s); break;
+    case 5: launch_tile<OP, 5, NP>(fast, a, grid, s); break;
+    case 6: launch_tile<OP, 6, NP>(fast, a, grid, s); break;
+    case 7: launch_tile<OP, 7, NP>(fast, a, grid, s); break;
+    case 8: launch_tile<OP, 8, NP>(fast, a, grid, s); break;
+    default: launch_tile<OP, 9, NP>(fast, a, grid, s); break;
   }
 }
 
-void launch_conv_bf16(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  if (op == OP_FWD) launch_op_bf16<OP_FWD>(tile, fast, a, grid, s);
-  else if (op == OP_DGRAD) launch_op_bf16<OP_DGRAD>(tile, fast, a, grid, s);
-  else launch_op_bf16<OP_WGRAD>(tile, fast, a, grid, s);
+template <int NP>
+static void launch_np(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
+  if (op == OP_FWD) launch_op_bf16<OP_FWD, NP>(tile, fast, a, grid, s);
+  else if (op == OP_DGRAD) launch_op_bf16<OP_DGRAD, NP>(tile, fast, a, grid, s);
+  else launch_op_bf16<OP_WGRAD, NP>(tile, fast, a, grid, s);
+}
+
+void launch_conv_bf16(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s, int np) {
+  if (np == 3) launch_np<3>(op, tile, fast, a, grid, s);
+  else launch_np<1>(op, tile, fast, a, grid, s);
 }
 
 }  // namespace jr

@@ -32,6 +32,8 @@ struct ConvArgs {
   // DGRAD phase (py,px): taps r = r0 + sh*a (a < na), c = c0 + sw*b (b < nb);
   // m = (b, u, v) over hc x wc; ih = sh*u + py; oh = u + ey - a.
   int py, px, r0, c0, na, nb, ey, ex, hc, wc;
+  // JR_F32_X8P: element stride between the h, m and l planes of A and of B
+  long long a_ps, b_ps;
 };
 
 // Output element offset of GEMM row m (column 0), or -1 to drop the row.
@@ -56,22 +58,17 @@ __device__ __forceinline__ long long out_row(const ConvArgs& g, int m) {
 // s_waitcnt vmcnt(n) + lgkmcnt(0) for a wave-uniform runtime n (immediate
 // operand: switch over the values a K-tile pipeline can need).
 __device__ __forceinline__ void wait_vmcnt(int n) {
+#define JR_VMCNT_CASE(k) case k: asm volatile("s_waitcnt vmcnt(" #k ") lgkmcnt(0)" ::: "memory"); break;
   switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory"); break;
+    JR_VMCNT_CASE(0) JR_VMCNT_CASE(1) JR_VMCNT_CASE(2) JR_VMCNT_CASE(3) JR_VMCNT_CASE(4) JR_VMCNT_CASE(5)
+    JR_VMCNT_CASE(6) JR_VMCNT_CASE(7) JR_VMCNT_CASE(8) JR_VMCNT_CASE(9) JR_VMCNT_CASE(10) JR_VMCNT_CASE(11)
+    JR_VMCNT_CASE(12) JR_VMCNT_CASE(13) JR_VMCNT_CASE(14) JR_VMCNT_CASE(15) JR_VMCNT_CASE(16) JR_VMCNT_CASE(17)
+    JR_VMCNT_CASE(18) JR_VMCNT_CASE(19) JR_VMCNT_CASE(20) JR_VMCNT_CASE(21) JR_VMCNT_CASE(22) JR_VMCNT_CASE(23)
+    JR_VMCNT_CASE(24) JR_VMCNT_CASE(25) JR_VMCNT_CASE(26) JR_VMCNT_CASE(27) JR_VMCNT_CASE(28) JR_VMCNT_CASE(29)
+    JR_VMCNT_CASE(30)
     default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
   }
+#undef JR_VMCNT_CASE
 }
 
 // Advance the mixed-radix counter (z, y, x) (radices ly, lx) by BK along x.
@@ -420,11 +417,34 @@ static constexpr TileCfg kCfgsBf16[] = {
     {128, 192, 2, 32, 3, 1.02},  // 5: wave 64x96, 60 KiB
     {128, 96, 4, 32, 3, 0.90},   // 6: wave 32x96, 42 KiB
     {64, 64, 2, 64, 3, 0.75},    // 7: wave 32x32, 48 KiB
+    // one block per CU, wave tiles of 128 x 128 / 128 x 96: 16 / 12 MFMAs per
+    // k-step against 4 DMA pieces per wave (0.25-0.33 DMA per MFMA, where the
+    // 64 x 64 wave tiles issue 0.5: the per-MFMA issue budget is the bound)
+    {256, 256, 2, 32, 3, 1.10},  // 8: wave 128x128, 96 KiB
+    {256, 192, 2, 32, 3, 1.08},  // 9: wave 128x96, 84 KiB
 };
 constexpr int kNumCfgsBf16 = sizeof(kCfgsBf16) / sizeof(kCfgsBf16[0]);
 
-// bf16 GEMM launch (jr_conv_bf16.hip): tile index into kCfgsBf16, fast =
-// the uniform-tap / single-carry kernel variant.
-void launch_conv_bf16(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s);
+// JR_F32_X8P tiles: the bf16 kernel with three operand planes (h, m, l) and
+// eight MFMAs per k-step, so BK = 16 (one k-step) already gives a wave
+// 8 * TM * TN MFMAs per K-tile; LDS = NBUF * 3 * (BM + BN) * BK * 2 B.
+static constexpr TileCfg kCfgsX8P[] = {
+    {128, 128, 2, 16, 3, 1.00},  // 0: wave 64x64, 72 KiB LDS
+    {128, 128, 2, 16, 4, 1.00},  // 1: 96 KiB
+    {256, 128, 2, 16, 3, 1.05},  // 2: wave 128x64, 108 KiB
+    {128, 64, 2, 16, 3, 0.92},   // 3: wave 64x32, 54 KiB
+    {256, 64, 4, 16, 3, 1.00},   // 4: wave 64x64, 81 KiB
+    {128, 192, 2, 16, 3, 1.02},  // 5: wave 64x96, 90 KiB
+    {128, 96, 4, 16, 3, 0.90},   // 6: wave 32x96, 63 KiB
+    {64, 64, 2, 32, 3, 0.75},    // 7: wave 32x32, 72 KiB
+    {256, 256, 2, 16, 2, 1.10},  // 8: wave 128x128, 96 KiB
+    {256, 192, 2, 16, 3, 1.08},  // 9: wave 128x96, 126 KiB
+};
+constexpr int kNumCfgsX8P = sizeof(kCfgsX8P) / sizeof(kCfgsX8P[0]);
+
+// bf16-operand GEMM launch (jr_conv_bf16.hip): tile index into kCfgsBf16
+// (np = 1, JR_BF16) or kCfgsX8P (np = 3, JR_F32_X8P), fast = the
+// uniform-tap / single-carry kernel variant.
+void launch_conv_bf16(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s, int np = 1);
 
 }  // namespace jr

@@ -175,7 +175,19 @@ static __device__ __forceinline__ int wprep_tiles(int kh, int kw, int cin, int c
   return kh * kw * ((((cin + 7) / 8 * 8) + 31) / 32) * ((cout + 31) / 32);
 }
 
-template <bool SINGLE>
+// Exact three-way split x = h + m + l into bf16 (JR_F32_X8P operands): the
+// terms of SplitFrag in jr_conv.hip, bit for bit (RNE casts; the remainders
+// are exact in fp32 and l is exact in bf16).
+__device__ __forceinline__ void split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+  h = f2bf(x);
+  const float r = __fsub_rn(x, bf2f(h));
+  m = f2bf(r);
+  l = f2bf(__fsub_rn(r, bf2f(m)));
+}
+
+// NP = 1: bf16 copies (JR_BF16); NP = 3: h / m / l planes, plane stride =
+// the layer's element count (JR_F32_X8P).
+template <bool SINGLE, int NP>
 __global__ void __launch_bounds__(256) k_wprep(const jr_wprep* __restrict__ table, jr_wprep one, int nl,
                                                const float* __restrict__ src, uint16_t* hwio, uint16_t* wt) {
   __shared__ float t[32][33];
@@ -197,22 +209,81 @@ __global__ void __launch_bounds__(256) k_wprep(const jr_wprep* __restrict__ tabl
   const int tap = local / (cit * cot), rem = local - tap * (cit * cot);
   const int ci0 = (rem / cot) * 32, co0 = (rem % cot) * 32;
   const float* s = src + L.src_off;
+  const int64_t hps = (int64_t)L.kh * L.kw * L.c_in * L.c_out;
+  const int64_t K = (int64_t)L.kh * L.kw * c8;
+  const int64_t tps = (int64_t)L.c_out * K;
   for (int e = threadIdx.x; e < 1024; e += 256) {
     const int ci = ci0 + (e >> 5), co = co0 + (e & 31);
     float v = 0.f;
     if (ci < L.c_in && co < L.c_out) {
       const int64_t idx = ((int64_t)tap * L.c_in + ci) * L.c_out + co;
       v = s[idx];
-      if (hwio) hwio[L.hwio_off + idx] = f2bf(v);
+      if (hwio) {
+        if constexpr (NP == 1) {
+          hwio[L.hwio_off + idx] = f2bf(v);
+        } else {
+          uint16_t h, m, l;
+          split3(v, h, m, l);
+          hwio[L.hwio_off + idx] = h;
+          hwio[L.hwio_off + hps + idx] = m;
+          hwio[L.hwio_off + 2 * hps + idx] = l;
+        }
+      }
     }
     t[e >> 5][e & 31] = v;
   }
   __syncthreads();
   if (!wt) return;
-  const int64_t K = (int64_t)L.kh * L.kw * c8;
   for (int e = threadIdx.x; e < 1024; e += 256) {
     const int co = co0 + (e >> 5), ci = ci0 + (e & 31);
-    if (co < L.c_out && ci < c8) wt[L.wt_off + co * K + (int64_t)tap * c8 + ci] = f2bf(t[e & 31][e >> 5]);
+    if (co < L.c_out && ci < c8) {
+      const int64_t o = L.wt_off + co * K + (int64_t)tap * c8 + ci;
+      const float v = t[e & 31][e >> 5];
+      if constexpr (NP == 1) {
+        wt[o] = f2bf(v);
+      } else {
+        uint16_t h, m, l;
+        split3(v, h, m, l);
+        wt[o] = h;
+        wt[o + tps] = m;
+        wt[o + 2 * tps] = l;
+      }
+    }
+  }
+}
+
+// Activation / gradient split: one thread per 4 channels of one row (c and
+// the offsets multiples of 4: float4 in, three 8-byte plane stores out),
+// else one per channel.  Channels [c, c_pad) of the destination get zeros.
+template <bool VEC>
+__global__ void __launch_bounds__(256) k_split_x8p(const float* __restrict__ src, int64_t rows, int c, int src_off,
+                                                   int src_stride, uint16_t* __restrict__ dst, int c_pad, int dst_off,
+                                                   int dst_stride, int64_t ps) {
+  constexpr int V = VEC ? 4 : 1;
+  const int per_row = (c_pad + V - 1) / V;
+  const int64_t total = rows * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / per_row;
+    const int ch = (int)(i - r * per_row) * V;
+    uint16_t* d = dst + r * dst_stride + dst_off + ch;
+    if constexpr (VEC) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ch < c) v = *reinterpret_cast<const float4*>(src + r * src_stride + src_off + ch);
+      const float x[4] = {v.x, v.y, v.z, v.w};
+      uint16_t h[4], m[4], l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) split3(x[k], h[k], m[k], l[k]);
+      *reinterpret_cast<uint2*>(d) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+      *reinterpret_cast<uint2*>(d + ps) = make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
+      *reinterpret_cast<uint2*>(d + 2 * ps) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+    } else {
+      const float x = ch < c ? src[r * src_stride + src_off + ch] : 0.f;
+      uint16_t h, m, l;
+      split3(x, h, m, l);
+      d[0] = h;
+      d[ps] = m;
+      d[2 * ps] = l;
+    }
   }
 }
 
@@ -226,8 +297,8 @@ JR_API int jr_conv_weights_bf16(const float* w, int32_t kh, int32_t kw, int32_t 
   const int tiles = jr_conv_weights_bf16_tiles(kh, kw, c_in, c_out);
   if (!w || tiles <= 0) return fail(JR_ERR_INVALID, "conv_weights_bf16: bad arguments");
   jr_wprep one{0, 0, 0, kh, kw, c_in, c_out, 0, 0};
-  hipLaunchKernelGGL(k_wprep<true>, dim3(tiles), dim3(256), 0, as_stream(stream), (const jr_wprep*)nullptr, one, 1,
-                     w, (uint16_t*)w_hwio, (uint16_t*)w_t);
+  hipLaunchKernelGGL((k_wprep<true, 1>), dim3(tiles), dim3(256), 0, as_stream(stream), (const jr_wprep*)nullptr, one,
+                     1, w, (uint16_t*)w_hwio, (uint16_t*)w_t);
   return check_launch("conv_weights_bf16");
 }
 
@@ -236,9 +307,46 @@ JR_API int jr_conv_weights_bf16_multi(const jr_wprep* layers, int32_t n_layers, 
   if (!layers || !src || n_layers <= 0 || total_tiles < 0) return fail(JR_ERR_INVALID, "conv_weights_bf16_multi: bad arguments");
   if (total_tiles == 0) return JR_OK;
   jr_wprep none{};
-  hipLaunchKernelGGL(k_wprep<false>, dim3(total_tiles), dim3(256), 0, as_stream(stream), layers, none, n_layers, src,
-                     (uint16_t*)hwio, (uint16_t*)wt);
+  hipLaunchKernelGGL((k_wprep<false, 1>), dim3(total_tiles), dim3(256), 0, as_stream(stream), layers, none, n_layers,
+                     src, (uint16_t*)hwio, (uint16_t*)wt);
   return check_launch("conv_weights_bf16_multi");
+}
+
+JR_API int jr_conv_weights_x8p(const float* w, int32_t kh, int32_t kw, int32_t c_in, int32_t c_out, void* w_hwio,
+                               void* w_t, void* stream) {
+  const int tiles = jr_conv_weights_bf16_tiles(kh, kw, c_in, c_out);
+  if (!w || tiles <= 0) return fail(JR_ERR_INVALID, "conv_weights_x8p: bad arguments");
+  jr_wprep one{0, 0, 0, kh, kw, c_in, c_out, 0, 0};
+  hipLaunchKernelGGL((k_wprep<true, 3>), dim3(tiles), dim3(256), 0, as_stream(stream), (const jr_wprep*)nullptr, one,
+                     1, w, (uint16_t*)w_hwio, (uint16_t*)w_t);
+  return check_launch("conv_weights_x8p");
+}
+
+JR_API int jr_conv_weights_x8p_multi(const jr_wprep* layers, int32_t n_layers, int32_t total_tiles, const float* src,
+                                     void* hwio, void* wt, void* stream) {
+  if (!layers || !src || n_layers <= 0 || total_tiles < 0) return fail(JR_ERR_INVALID, "conv_weights_x8p_multi: bad arguments");
+  if (total_tiles == 0) return JR_OK;
+  jr_wprep none{};
+  hipLaunchKernelGGL((k_wprep<false, 3>), dim3(total_tiles), dim3(256), 0, as_stream(stream), layers, none, n_layers,
+                     src, (uint16_t*)hwio, (uint16_t*)wt);
+  return check_launch("conv_weights_x8p_multi");
+}
+
+JR_API int jr_split_x8p(const float* src, int64_t rows, int32_t c, int32_t src_off, int32_t src_stride, void* dst,
+                        int32_t c_pad, int32_t dst_off, int32_t dst_stride, int64_t plane_stride, void* stream) {
+  if (!src || !dst || rows < 0 || c <= 0 || c_pad < c || src_off < 0 || src_off + c > src_stride || dst_off < 0 ||
+      dst_off + c_pad > dst_stride || plane_stride < rows * dst_stride)
+    return fail(JR_ERR_INVALID, "split_x8p: bad arguments");
+  if (rows == 0) return JR_OK;
+  const bool vec = c % 4 == 0 && c_pad % 4 == 0 && src_off % 4 == 0 && src_stride % 4 == 0 && dst_off % 4 == 0 &&
+                   dst_stride % 4 == 0 && plane_stride % 4 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 7) == 0;
+  if (vec)
+    hipLaunchKernelGGL(k_split_x8p<true>, dim3(grid_for(rows * (c_pad / 4))), dim3(256), 0, as_stream(stream), src, rows,
+                       c, src_off, src_stride, (uint16_t*)dst, c_pad, dst_off, dst_stride, plane_stride);
+  else
+    hipLaunchKernelGGL(k_split_x8p<false>, dim3(grid_for(rows * c_pad)), dim3(256), 0, as_stream(stream), src, rows, c,
+                       src_off, src_stride, (uint16_t*)dst, c_pad, dst_off, dst_stride, plane_stride);
+  return check_launch("split_x8p");
 }
 
 JR_API int jr_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream) {

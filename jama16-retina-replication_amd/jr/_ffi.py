@@ -18,6 +18,7 @@ JR_OK = 0
 JR_F32 = 0
 JR_BF16 = 1
 JR_F32_X8 = 2      # conv entry points only: fp32 tensors, bf16x8-split MFMA products (jr.h)
+JR_F32_X8P = 3     # conv entry points only: the X8 arithmetic on pre-split h/m/l bf16 operand planes (jr.h)
 JR_CONV_FWD, JR_CONV_BWD_DATA, JR_CONV_BWD_FILTER = 0, 1, 2
 JR_HEAD_SIGMOID, JR_HEAD_SOFTMAX = 0, 1
 
@@ -72,6 +73,12 @@ _SIGS = {
                                      c_void_p]),
     "jr_conv_weights_bf16_multi": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                            c_void_p]),
+    "jr_conv_weights_x8p": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                    c_void_p]),
+    "jr_conv_weights_x8p_multi": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                          c_void_p]),
+    "jr_split_x8p": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_int32, c_int32, c_int32,
+                             c_int64, c_void_p]),
     "jr_bn_workspace_size": (c_size_t, [c_int64, c_int32]),
     "jr_bn_stats": (c_int, [c_int, c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
                             c_void_p, c_size_t, c_void_p]),
