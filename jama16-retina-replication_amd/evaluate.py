@@ -7,6 +7,13 @@ Multi-GPU: torchrun --nproc-per-node N evaluate.py ... shards whole batches
 (dataset order, so every BN batch is the reference's, App. C Q1) across
 ranks with no collective on the data path; rank 0 gathers the [N] per-model
 predictions, averages and scores them.
+
+The reference restores and runs one member at a time, re-reading and
+re-decoding the test set per member (evaluate.py:166-211).  Here every
+member is resident on the GPU at once (one engine each: parameters plus
+batch-32 buffers, a few GB per member against 288 GB of HBM), and each test
+batch is decoded once and run through all members -- the same batches, so
+the same batch-statistics BN (App. C Q1) and the same predictions.
 """
 import argparse
 import csv
@@ -52,55 +59,83 @@ def build_parser():
                    help="path to where operating points metrics should be saved")
     p.add_argument("-b", "--batch_size", default=DEFAULT_BATCH_SIZE, help="batch size")
     p.add_argument("-op", "--operating_threshold", default=0.5, help="operating threshold")
-    p.add_argument("--conv_math", default="x8", choices=["x8", "f32"],
+    p.add_argument("--conv_math", default="x8", choices=["x8", "x8p", "f32"],
                    help="fp32 convolution arithmetic: x8 = exact 3-way bf16 split on the matrix cores (fp32-accurate, "
-                        "default), f32 = fp32 MFMA")
+                        "default), x8p = the same on pre-split operand planes, f32 = fp32 MFMA")
     return p
 
 
 def expand_model_paths(load_model_path: str):
     """evaluate.py:74-83: comma list, or glob when the path holds '*', '+'
-    or '?' (each match's last extension stripped, duplicates removed)."""
+    or '?' (each match's last extension stripped, duplicates removed).  Stems
+    that are not complete checkpoints (a leftover `.data-*.tmp` of an
+    interrupted save strips to `<path>.data-00000-of-00001`) are dropped."""
+    from jr import checkpoint
     if "," in load_model_path:
         return load_model_path.split(",")
     if any(ch in load_model_path for ch in "*+?"):
         stems = {".".join(x.split(".")[:-1]) for x in glob("{}*".format(load_model_path))}
-        return sorted(stems)
+        return sorted(s for s in stems if checkpoint.exists(s))
     return [load_model_path]
 
 
-def predict_all(engine, paths, data_dir, batch_size, rank=0, world=1):
-    """Per-model predictions over this rank's batches: ([M][n_r, 1], [n_r, 1],
-    batch indices)."""
+def make_engines(paths, meta, batch_size, device=0, conv_math="x8"):
+    """One inference engine per ensemble member, parameters loaded; the first
+    autotunes the conv tiles, the others reuse them (libjr's tile cache is
+    per geometry)."""
     from jr import checkpoint
+    from jr.engine import Engine
+    engines = []
+    for k, path in enumerate(paths):
+        eng = Engine(batch_size, meta["height"], meta["width"], meta.get("units", 1), device=device,
+                     train=False, conv_math=conv_math, autotune=(k == 0))
+        flat, _ = checkpoint.load(path, eng.g)
+        eng.load_params(flat)
+        engines.append(eng)
+    return engines
+
+
+def predict_all(engines, data_dir, batch_size, rank=0, world=1):
+    """Per-member predictions over this rank's batches: ([M][n_r, 1], [n_r, 1],
+    batch indices).  Each batch is decoded once (this rank's batches only)
+    and run through every member."""
     from jr.session import Session
-    sess = Session(engine)
+    sessions = [Session(e) for e in engines]
     dataset = lib.dataset.initialize_dataset(
         data_dir, batch_size, num_workers=NUM_WORKERS, prefetch_buffer_size=2 * batch_size,
         image_data_format="channels_last", num_channels=NUM_CHANNELS,
-        image_dim=[engine.g.height, engine.g.width], decode_dtype="uint8")
-    preds, labels, order = [], None, None
-    for path in paths:
-        flat, _ = checkpoint.load(path, engine.g)
-        engine.load_params(flat)
-        got_y = []
-        ids = []
+        image_dim=[engines[0].g.height, engines[0].g.width], decode_dtype="uint8",
+        shard=(rank, world))
+    preds = [[] for _ in engines]
+    got_y, ids = [], []
+    it = iter(dataset)
+    try:
+        for k, (x, y) in enumerate(it):
+            ids.append(k * world + rank)
+            got_y.append(y)
+            for m, sess in enumerate(sessions):
+                out = lib.evaluation.perform_test(sess=sess, init_op=None, feed_dict_fn=_one_batch(x, y),
+                                                  custom_tensors=["predictions"])
+                preds[m].append(out[0])
+    finally:
+        lib.dataset.close_iterator(it)
+    empty = np.zeros((0, 1), np.float32)
+    preds = [np.vstack(p) if p else empty for p in preds]
+    labels = np.vstack(got_y) if got_y else empty
+    return preds, labels, ids
 
-        def feed(it=iter(enumerate(dataset))):
-            while True:
-                i, (x, y) = next(it)
-                if i % world == rank:
-                    ids.append(i)
-                    got_y.append(y)
-                    return {"x": x, "y": y}
 
-        out = lib.evaluation.perform_test(sess=sess, init_op=None, feed_dict_fn=feed,
-                                          custom_tensors=["predictions"])
-        preds.append(out[0])
-        if labels is None:                 # labels from the first model (evaluate.py:116-117,211)
-            labels = np.vstack(got_y) if got_y else np.zeros((0, 1), np.float32)
-            order = list(ids)
-    return preds, labels, order
+def _one_batch(x, y):
+    """feed_dict_fn for lib.evaluation.perform_test: one batch, then the end
+    of the pass (evaluate.py:114-118 feed_images)."""
+    state = {"done": False}
+
+    def feed():
+        if state["done"]:
+            raise StopIteration
+        state["done"] = True
+        return {"x": x, "y": y}
+    return feed
 
 
 def main(argv=None):
@@ -124,7 +159,6 @@ def main(argv=None):
 
     import torch
     from jr import checkpoint
-    from jr.engine import Engine
 
     load_model_paths = expand_model_paths(str(args.load_model_path))
     batch_size = int(args.batch_size)
@@ -153,10 +187,9 @@ Using operating treshold: {},
         print("Trying to load model(s):\n{}".format("\n".join(load_model_paths)))
 
     thresholds = lib.metrics.generate_thresholds(NUM_THRESHOLDS, KEPSILON) + [operating_threshold]
-    _, meta = checkpoint.load(load_model_paths[0])
-    engine = Engine(batch_size, meta["height"], meta["width"], meta.get("units", 1), device=local,
-                    train=False, conv_math=args.conv_math)
-    preds, labels, order = predict_all(engine, load_model_paths, data_dir, batch_size, rank, world)
+    meta = checkpoint.read_meta(load_model_paths[0])
+    engines = make_engines(load_model_paths, meta, batch_size, device=local, conv_math=args.conv_math)
+    preds, labels, order = predict_all(engines, data_dir, batch_size, rank, world)
 
     if dist:   # gather every rank's batches to rank 0, restore dataset order
         gathered = [None] * world

@@ -72,5 +72,15 @@ def load(path: str, graph=None, verify: bool = True) -> Tuple[np.ndarray, dict]:
     return flat, meta
 
 
+def read_meta(path: str) -> dict:
+    """The graph configuration of a checkpoint, from <path>.meta only (no
+    parameter read or checksum): what evaluate.py needs to size its engines."""
+    with open(path + ".meta") as f:
+        meta = json.load(f)
+    if meta.get("format") != FORMAT:
+        raise ValueError(f"{path}: not a {FORMAT} checkpoint")
+    return meta
+
+
 def exists(path: str) -> bool:
     return all(os.path.exists(path + s) for s in (".meta", ".index", DATA_SUFFIX))

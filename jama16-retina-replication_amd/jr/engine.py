@@ -52,9 +52,9 @@ class Engine:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if conv_math is None:            # fp32 default: x8 (fp32-accurate, on the bf16 matrix cores)
             conv_math = "x8" if dtype == "f32" else "bf16"
-        if (dtype == "f32" and conv_math not in ("f32", "x8")) or (dtype == "bf16" and conv_math != "bf16"):
-            raise ValueError("conv_math: 'x8' or 'f32' for dtype f32 (x8 = JR_F32_X8, f32 = fp32 MFMA); "
-                             "'bf16' for dtype bf16")
+        if (dtype == "f32" and conv_math not in ("f32", "x8", "x8p")) or (dtype == "bf16" and conv_math != "bf16"):
+            raise ValueError("conv_math: 'x8', 'x8p' or 'f32' for dtype f32 (x8 = JR_F32_X8, x8p = JR_F32_X8P "
+                             "on pre-split operand planes, f32 = fp32 MFMA); 'bf16' for dtype bf16")
         if not torch.cuda.is_available():
             raise RuntimeError("jr.Engine needs a ROCm GPU (libjr has no CPU path)")
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
@@ -68,7 +68,8 @@ class Engine:
         # fp32 and forms the GEMM products on the bf16 matrix cores from an
         # exact three-way split (jr.h); everything else runs self.dt
         self.conv_math = conv_math
-        self.cdt = _ffi.JR_F32_X8 if conv_math == "x8" else self.dt
+        self.x8p = conv_math == "x8p"
+        self.cdt = {"x8": _ffi.JR_F32_X8, "x8p": _ffi.JR_F32_X8P}.get(conv_math, self.dt)
         self.train_mode = train
         self.optimizer = optimizer
         self.lr = float(lr)
@@ -150,8 +151,10 @@ class Engine:
                               for _ in range(self.nlanes)]
             self.draw = self.draw_lane[0]
             self.dfeat = self._t(B * feat_c)
-        if self.dt == _ffi.JR_BF16:
-            self._alloc_bf16_filters()
+        if self.dt == _ffi.JR_BF16 or self.x8p:
+            self._alloc_bf16_filters(planes=3 if self.x8p else 1)
+        if self.x8p:
+            self._alloc_planes()
         ws = 0
         for u in self.cunits:
             d = self._conv_desc(u, B)
@@ -164,12 +167,35 @@ class Engine:
         self.ws_lane = [self._t((self.ws_bytes + 15) // 4 + 4) for _ in range(self.nlanes)]
         self.ws = self.ws_lane[0]
 
-    def _alloc_bf16_filters(self) -> None:
+    def _alloc_planes(self) -> None:
+        """JR_F32_X8P operand planes (jr.h): the exact bf16 h/m/l split of
+        every conv input buffer (written once per step by jr_split_x8p when
+        the buffer is complete, read by the forward and the filter-gradient
+        GEMMs) and of each lane's raw-output gradient scratch (dgrad and
+        wgrad operand).  Channel radices are padded to 8 (the image: 3 -> 8)."""
+        g, B = self.g, self.batch
+        bf = torch.bfloat16
+        self.plane_c = {}
+        self.aplanes = {}
+        for u in self.cunits:
+            b = g.bufs[u.x]
+            if u.x in self.aplanes:
+                continue
+            cp = (b.c + 7) // 8 * 8
+            self.plane_c[u.x] = cp
+            self.aplanes[u.x] = self._t(3 * B * b.h * b.w * cp, bf)
+        if self.train_mode:
+            n = max(B * u.ho * u.wo * u.cout for u in self.cunits)
+            self.drawp_lane = [self._t(3 * n, bf) for _ in range(self.nlanes)]
+
+    def _alloc_bf16_filters(self, planes: int = 1) -> None:
         """bf16 operand copies of every conv launch's kernel (block), refreshed
         from the fp32 master parameters by ONE jr_conv_weights_bf16_multi
         launch at the start of each forward: HWIO (bwd_data) and
-        W^T [co][kh][kw][c8] (fwd)."""
+        W^T [co][kh][kw][c8] (fwd).  planes = 3 (JR_F32_X8P): each copy is
+        the three bf16 planes of the exact split, jr_conv_weights_x8p_multi."""
         L = self.lib
+        self.wplanes = planes
         layers, tiles = [], 0
         self.wb_hwio_off, self.wb_t_off = {}, {}
         ho = to = 0
@@ -178,9 +204,11 @@ class Engine:
             layers.append(_ffi.WPrep(u.koff, ho, to, u.kh, u.kw, u.cin, u.cout, tiles, 0))
             self.wb_hwio_off[u.first.idx], self.wb_t_off[u.first.idx] = ho, to
             tiles += L.jr_conv_weights_bf16_tiles(u.kh, u.kw, u.cin, u.cout)
-            # 16 B-aligned starts (8 bf16)
-            ho += (u.kh * u.kw * u.cin * u.cout + 7) // 8 * 8
-            to += u.cout * u.kh * u.kw * c8
+            # 16 B-aligned starts (8 bf16); x8p: three planes per layer, plane
+            # stride = the layer's element count (jr.h)
+            hw_n = u.kh * u.kw * u.cin * u.cout
+            ho += (planes * hw_n + 7) // 8 * 8
+            to += planes * u.cout * u.kh * u.kw * c8
         arr = (_ffi.WPrep * len(layers))(*layers)
         self.wprep_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
         self.wprep_layers, self.wprep_tiles = len(layers), tiles
@@ -188,19 +216,20 @@ class Engine:
         self.w_t = self._t(to, torch.bfloat16)
 
     def _wprep_call(self, stream=None):
-        return (self.lib.jr_conv_weights_bf16_multi,
+        fn = self.lib.jr_conv_weights_x8p_multi if self.wplanes == 3 else self.lib.jr_conv_weights_bf16_multi
+        return (fn,
                 (self.wprep_table.data_ptr(), self.wprep_layers, self.wprep_tiles, self.params.data_ptr(),
                  self.w_hwio.data_ptr(), self.w_t.data_ptr(), stream or self._s), "wprep_bf16")
 
     def _wf(self, u: ConvUnit) -> int:
-        """Filter operand of conv fwd: fp32 HWIO master block, or its bf16 W^T copy."""
-        if self.dt == _ffi.JR_BF16:
+        """Filter operand of conv fwd: fp32 HWIO master block, or its bf16 W^T copy (planes)."""
+        if self.dt == _ffi.JR_BF16 or self.x8p:
             return self.w_t.data_ptr() + 2 * self.wb_t_off[u.first.idx]
         return self.params.data_ptr() + 4 * u.koff
 
     def _wd(self, u: ConvUnit) -> int:
-        """Filter operand of conv bwd_data: fp32 HWIO master block, or its bf16 copy."""
-        if self.dt == _ffi.JR_BF16:
+        """Filter operand of conv bwd_data: fp32 HWIO master block, or its bf16 copy (planes)."""
+        if self.dt == _ffi.JR_BF16 or self.x8p:
             return self.w_hwio.data_ptr() + 2 * self.wb_hwio_off[u.first.idx]
         return self.params.data_ptr() + 4 * u.koff
 
@@ -212,23 +241,24 @@ class Engine:
         L, B = self.lib, self.batch
         ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
         s = self._s
-        if self.dt == _ffi.JR_BF16:
+        if self.dt == _ffi.JR_BF16 or self.x8p:
             fn, args, name = self._wprep_call()
             _ffi.check(name, fn(*args))
         for u in self.cunits:
             d = self._conv_desc(u, B)
-            x = self.acts[u.x].data_ptr()
+            x = (self.aplanes[u.x] if self.x8p else self.acts[u.x]).data_ptr()
+            draw = (self.drawp_lane[0] if self.x8p else self.draw).data_ptr() if self.train_mode else 0
             raw = self.raw_unit[u.first.idx].data_ptr()
             _ffi.check("autotune fwd", L.jr_conv2d_autotune(ctypes.byref(d), _ffi.JR_CONV_FWD, self.cdt, x,
                                                              self._wf(u), raw, ws, wsb, s))
             if not self.train_mode:
                 continue
             _ffi.check("autotune wgrad", L.jr_conv2d_autotune(
-                ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, self.cdt, x, self.draw.data_ptr(),
+                ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER, self.cdt, x, draw,
                 self.grads.data_ptr() + 4 * u.koff, ws, wsb, s))
             if u.x != self.g.input_buf:
                 _ffi.check("autotune dgrad", L.jr_conv2d_autotune(
-                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.cdt, self.draw.data_ptr(), self._wd(u),
+                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.cdt, draw, self._wd(u),
                     self.dacts[u.x].data_ptr(), ws, wsb, s))
         self.synchronize()
         if self.train_mode:
@@ -245,6 +275,47 @@ class Engine:
                   for p in range(u.stride * u.stride)]
             out[u.name] = (f, wg, dg)
         return out
+
+    def tile_table(self) -> dict:
+        """The conv tile configuration of every launch, as saved in checkpoint
+        meta (jr.checkpoint) and accepted back by set_tile_table: with the
+        same table two runs sum in the same order (bitwise-equal steps on any
+        MI355X).  Keyed by conv math, batch and resolution."""
+        return {"conv_math": self.conv_math, "batch": self.batch, "height": self.g.height,
+                "width": self.g.width, "configs": {k: [f, wg, list(dg)] for k, (f, wg, dg) in
+                                                   self.conv_configs().items()}}
+
+    def set_tile_table(self, table: dict) -> None:
+        """Pin every conv launch to the configs of `table` (tile_table())."""
+        if (table.get("conv_math"), table.get("batch"), table.get("height"), table.get("width")) != \
+                (self.conv_math, self.batch, self.g.height, self.g.width):
+            raise ValueError("tile table is for another conv math / batch / resolution")
+        cfgs = table["configs"]
+        for u in self.cunits:
+            f, wg, dg = cfgs[u.name]
+            d = self._conv_desc(u, self.batch)
+            _ffi.check("set_config", self.lib.jr_conv2d_set_config(ctypes.byref(d), _ffi.JR_CONV_FWD, self.cdt, 0, f))
+            if not self.train_mode:
+                continue
+            _ffi.check("set_config", self.lib.jr_conv2d_set_config(ctypes.byref(d), _ffi.JR_CONV_BWD_FILTER,
+                                                                   self.cdt, 0, wg))
+            if u.x != self.g.input_buf:
+                for p, c in enumerate(dg):
+                    _ffi.check("set_config", self.lib.jr_conv2d_set_config(ctypes.byref(d), _ffi.JR_CONV_BWD_DATA,
+                                                                           self.cdt, p, c))
+
+    def clear_tile_table(self) -> None:
+        """Back to the deterministic planner heuristic for every conv launch
+        (drops autotuned or pinned configs of this engine's geometries)."""
+        for u in self.cunits:
+            d = self._conv_desc(u, self.batch)
+            ops = [(_ffi.JR_CONV_FWD, 0)]
+            if self.train_mode:
+                ops.append((_ffi.JR_CONV_BWD_FILTER, 0))
+                if u.x != self.g.input_buf:
+                    ops += [(_ffi.JR_CONV_BWD_DATA, p) for p in range(u.stride * u.stride)]
+            for op, p in ops:
+                _ffi.check("set_config", self.lib.jr_conv2d_set_config(ctypes.byref(d), op, self.cdt, p, -1))
 
     # ------------------------------------------------------------ parameters
     def load_params(self, flat: np.ndarray) -> None:
@@ -272,7 +343,10 @@ class Engine:
 
     # ------------------------------------------------------------ descriptors
     def _conv_desc(self, u: ConvUnit, B: int) -> _ffi.ConvDesc:
-        xs = self.in_stride if u.x == self.g.input_buf else u.cin
+        if self.x8p:          # x describes the operand planes: channel radix padded to 8
+            xs = (u.cin + 7) // 8 * 8
+        else:
+            xs = self.in_stride if u.x == self.g.input_buf else u.cin
         return _ffi.ConvDesc(B, u.h, u.w, u.cin, u.cout, u.kh, u.kw, u.stride, u.stride,
                              u.pad_h, u.pad_w, u.ho, u.wo, 0, xs, 0, u.cout)
 
@@ -316,9 +390,15 @@ class Engine:
         d_all = lambda b: [("d", b, o) for o in sorted(slices[b])]  # noqa: E731
         A = lambda bid: self.acts[bid].data_ptr()  # noqa: E731
         unit_of = self.plan.unit_of
-        wkey = ("w16",) if dt == _ffi.JR_BF16 else ("p",)
-        if dt == _ffi.JR_BF16:
+        x8p = self.x8p
+        wkey = ("w16",) if (dt == _ffi.JR_BF16 or x8p) else ("p",)
+        if dt == _ffi.JR_BF16 or x8p:
             add(fwd, *self._wprep_call(S[0]), 0, [("p",)], [("w16",)])
+        # x8p: conv operands are the split planes of the input buffer, written
+        # once (by the lane of its first consumer) when the buffer is complete
+        AX = (lambda bid: self.aplanes[bid].data_ptr()) if x8p else A  # noqa: E731
+        ax_reads = (lambda bid: [("ap", bid)]) if x8p else a_all  # noqa: E731
+        split_done = set()
         for i, n in enumerate(g.nodes):
             ln = lane_of[i]
             s, ws = S[ln], WS[ln]
@@ -331,11 +411,20 @@ class Engine:
                 M = B * u.ho * u.wo
                 uid = u.first.idx
                 raw = self.raw_unit[uid].data_ptr()
+                if x8p and u.x not in split_done:
+                    split_done.add(u.x)
+                    b = g.bufs[u.x]
+                    cp = self.plane_c[u.x]
+                    rows = B * b.h * b.w
+                    src_stride = self.in_stride if u.x == g.input_buf else b.c
+                    add(fwd, L.jr_split_x8p, (A(u.x), rows, b.c, 0, src_stride, AX(u.x), cp, 0, cp,
+                                              self.batch * b.h * b.w * cp, s),
+                        "split_x8p", ln, a_all(u.x), [("ap", u.x)])
                 # conv + the BN batch statistics of its raw output, fused
-                add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), cdt, A(u.x), self._wf(u), raw, BN_EPS,
+                add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), cdt, AX(u.x), self._wf(u), raw, BN_EPS,
                                                     self.mean_unit[uid].data_ptr(),
                                                     self.invstd_unit[uid].data_ptr(), ws, wsb, s),
-                    "conv_fwd", ln, a_all(u.x) + [wkey], [("r", uid), ("ws", ln)])
+                    "conv_fwd", ln, ax_reads(u.x) + [wkey], [("r", uid), ("ws", ln)])
                 for m, co in zip(u.members, u.col_off):
                     yb = g.bufs[m.y.buf]
                     add(fwd, L.jr_bn_relu_apply, (dt, raw, co, u.cout, M, m.cout, self.mean[m.idx].data_ptr(),
@@ -393,13 +482,19 @@ class Engine:
                                                     self._gp(f"batch_normalization_{m.idx + 1}/beta"), ws, wsb, s),
                             "bn_relu_bwd", ln, [("d", m.y.buf, m.y.c_off), ("r", uid), ("p",)],
                             [("draw", ln), ("g", uid), ("ws", ln)])
-                    add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), cdt, A(u.x), draw,
+                    dkey = ("draw", ln)
+                    if x8p:             # the raw-output gradient as split planes (dgrad and wgrad operand)
+                        drawp = self.drawp_lane[ln].data_ptr()
+                        add(bwd, L.jr_split_x8p, (draw, M, u.cout, 0, u.cout, drawp, u.cout, 0, u.cout, M * u.cout, s),
+                            "split_x8p", ln, [("draw", ln)], [("drawp", ln)])
+                        draw, dkey = drawp, ("drawp", ln)
+                    add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), cdt, AX(u.x), draw,
                                                       self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
-                        "conv_wgrad", ln, a_all(u.x) + [("draw", ln)], [("g", uid), ("ws", ln)])
+                        "conv_wgrad", ln, ax_reads(u.x) + [dkey], [("g", uid), ("ws", ln)])
                     if u.x != g.input_buf:
                         add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), cdt, draw, self._wd(u), D(u.x), acc, ws, wsb,
                                                         s),
-                            "conv_dgrad", ln, [("draw", ln), wkey], d_all(u.x) + [("ws", ln)])
+                            "conv_dgrad", ln, [dkey, wkey], d_all(u.x) + [("ws", ln)])
                         written.add(u.x)
                     bwd.append(Call("param_ready", u.koff, "hook", 0))
                 elif n.kind == "maxpool":

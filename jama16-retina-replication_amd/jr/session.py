@@ -32,6 +32,31 @@ class Session:
             "auc": M.create_reset_metric(M.auc, scope="auc"),
         }
         self.global_step = 0
+        # data-parallel ranks: reduce(vec float64) -> elementwise sum over ranks
+        self.reduce = None
+
+    def sync_metrics(self, *names) -> None:
+        """Sum the streaming states of `names` over the ranks (collective: every
+        rank calls it at the same point).  The states are counts and sums
+        (tp/fp/fn/tn at thresholds, the AUC's own confusion counts, Brier
+        total and count), so the reduced state is the state of one pass over
+        every rank's batches, and every rank then reads the same value."""
+        if self.reduce is None:
+            return
+        objs = [self.metrics[n][0].__self__ for n in names]
+        parts = []
+        for o in objs:
+            parts += [np.ravel(o.acc)] if hasattr(o, "acc") else [np.array([o.total, o.count])]
+        vec = self.reduce(np.concatenate(parts).astype(np.float64))
+        k = 0
+        for o in objs:
+            if hasattr(o, "acc"):
+                n = o.acc.size
+                o.acc = vec[k:k + n].reshape(o.acc.shape).astype(np.float32)
+            else:
+                n = 2
+                o.total, o.count = np.float32(vec[k]), np.float32(vec[k + 1])
+            k += n
 
     # ------------------------------------------------------------ metrics
     def reset(self, *names):

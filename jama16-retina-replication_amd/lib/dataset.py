@@ -20,9 +20,13 @@ threads (Pillow releases the GIL in its libjpeg decoder); prefetch runs the
 pipeline on a background thread.
 
 Extras (keyword-only, default off): `seed` for a reproducible shuffle (the
-reference's is unseeded, App. C Q4) and `decode_dtype='uint8'` to hand the
+reference's is unseeded, App. C Q4), `decode_dtype='uint8'` to hand the
 GPU the undecoded-scale bytes (libjr scales by 1/255 on device, 4x less
-host->device traffic; values are bit-identical).
+host->device traffic; values are bit-identical), and `shard=(rank, world)`
+for data-parallel ranks: every rank walks the same (seeded) stream of record
+handles and batches, and decodes only the batches b with b % world == rank
+-- the per-record JPEG work is split across ranks, the batch composition is
+that of the single-process stream.
 
 JPEG decoding [TF-3P]: TF's decode_jpeg defaults to libjpeg's IFAST DCT;
 Pillow uses ISLOW.  Pixels may differ by a few LSB from TF's decode — noted
@@ -85,9 +89,14 @@ class Dataset:
 
     def __init__(self, files: List[str], batch_size: int, num_epochs: int, num_workers: int,
                  prefetch_buffer_size: Optional[int], shuffle_buffer_size: Optional[int],
-                 image_dim: List[int], seed: Optional[int], decode_dtype: str):
+                 image_dim: List[int], seed: Optional[int], decode_dtype: str,
+                 shard: Optional[Tuple[int, int]] = None):
         if batch_size <= 0:
             raise ValueError("batch_size must be positive")
+        rank, world = shard or (0, 1)
+        if world < 1 or not 0 <= rank < world:
+            raise ValueError(f"bad shard {shard!r}: need 0 <= rank < world")
+        self.shard = (int(rank), int(world))
         self.files = files
         self.batch_size = int(batch_size)
         self.num_epochs = num_epochs
@@ -96,7 +105,9 @@ class Dataset:
         self.shuffle_buffer_size = shuffle_buffer_size
         self.image_dim = list(image_dim)
         self.decode_dtype = decode_dtype
+        self._seed = seed
         self._rng = np.random.default_rng(seed)
+        self._iteration = 0
 
     # ------------------------------------------------------------- stages
     def _items(self) -> Iterator[Tuple["tfrecord.RecordFile", int]]:
@@ -119,20 +130,21 @@ class Dataset:
         if n is None:
             yield from it
             return
+        rng = self._iter_rng
         buf = []
         for x in it:
             if len(buf) < n:
                 buf.append(x)
                 continue
-            i = int(self._rng.integers(len(buf)))
+            i = int(rng.integers(len(buf)))
             out, buf[i] = buf[i], x
             yield out
         while buf:
-            i = int(self._rng.integers(len(buf)))
+            i = int(rng.integers(len(buf)))
             buf[i], buf[-1] = buf[-1], buf[i]
             yield buf.pop()
 
-    def _item_batches(self) -> Iterator[list]:
+    def _all_item_batches(self) -> Iterator[list]:
         """repeat(num_epochs) then batch(batch_size), partial last batch kept."""
         epochs = self.num_epochs
         e = 0
@@ -150,6 +162,13 @@ class Dataset:
                 break
         if cur:
             yield cur
+
+    def _item_batches(self) -> Iterator[list]:
+        """This rank's batches (shard): handles only, before any decode."""
+        rank, world = self.shard
+        for b, items in enumerate(self._all_item_batches()):
+            if b % world == rank:
+                yield items
 
     def _decode_rows(self, items, rows, out) -> None:
         """map(_parse_example) for rows [rows) of one batch, written in place."""
@@ -201,10 +220,22 @@ class Dataset:
                         fu.cancel()
 
     def __iter__(self):
+        # seeded: iteration k shuffles with PCG64(seed, k) (tf.data's
+        # reshuffle_each_iteration with a seed), so ranks that stop an epoch
+        # early at different stream positions still agree on the next one;
+        # unseeded: one process-wide stream, as the reference's
+        self._iter_rng = (np.random.default_rng([self._seed, self._iteration]) if self._seed is not None
+                          else self._rng)
+        self._iteration += 1
         gen = self._batches()
         if not self.prefetch_buffer_size:
             return gen
         return _Prefetch(gen, max(1, int(self.prefetch_buffer_size) // self.batch_size + 1))
+
+    def num_batches(self) -> int:
+        """Batches of one pass over the whole (unsharded) stream."""
+        n = self.num_records() * max(1, self.num_epochs or 1)
+        return -(-n // self.batch_size)
 
     def num_records(self) -> int:
         n = 0
@@ -223,7 +254,12 @@ def _collect(entry):
 
 
 class _Prefetch:
-    """prefetch(): run the pipeline ahead on a background thread."""
+    """prefetch(): run the pipeline ahead on a background thread.
+
+    close() (also on garbage collection, and implied by reaching the end)
+    stops the thread at its next hand-off and closes the pipeline generator
+    on that thread, so its decode pool and mmap'd files are released when a
+    consumer stops early (a capped epoch, a `break`)."""
 
     _END = object()
 
@@ -234,27 +270,35 @@ class _Prefetch:
         self._t = threading.Thread(target=self._run, args=(gen,), daemon=True)
         self._t.start()
 
+    def _put(self, item) -> bool:
+        while not self._stop.is_set():
+            try:
+                self._q.put(item, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
     def _run(self, gen):
         try:
             for item in gen:
-                while not self._stop.is_set():
-                    try:
-                        self._q.put(item, timeout=0.1)
-                        break
-                    except queue.Full:
-                        continue
-                if self._stop.is_set():
-                    return
+                if not self._put(item):
+                    break
         except BaseException as e:  # surfaced to the consumer
             self._err = e
-        self._q.put(self._END)
+        finally:
+            gen.close()             # runs the pipeline's finally: decode pool shutdown
+        self._put(self._END)
 
     def __iter__(self):
         return self
 
     def __next__(self):
+        if self._stop.is_set():
+            raise StopIteration
         item = self._q.get()
         if item is self._END:
+            self._stop.set()
             if self._err is not None:
                 raise self._err
             raise StopIteration
@@ -262,6 +306,20 @@ class _Prefetch:
 
     def close(self):
         self._stop.set()
+        try:                        # unblock a producer waiting on a full queue
+            while True:
+                self._q.get_nowait()
+        except queue.Empty:
+            pass
+
+    def join(self, timeout=None):
+        self._t.join(timeout)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def initialize_dataset(image_dir, batch_size, num_epochs=1,
@@ -269,7 +327,7 @@ def initialize_dataset(image_dir, batch_size, num_epochs=1,
                        shuffle_buffer_size=None,
                        image_data_format='channels_last',
                        num_channels=3, image_dim=[299, 299], *,
-                       seed=None, decode_dtype="float32"):
+                       seed=None, decode_dtype="float32", shard=None):
     """lib/dataset.py:31-59 (same arguments, same order, same defaults)."""
     files = _tfrecord_files_from_folder(image_dir)
     if image_data_format == 'channels_first':
@@ -281,4 +339,11 @@ def initialize_dataset(image_dir, batch_size, num_epochs=1,
     if decode_dtype not in ("float32", "uint8"):
         raise ValueError("decode_dtype must be 'float32' or 'uint8'")
     return Dataset(files, batch_size, num_epochs, num_workers, prefetch_buffer_size,
-                   shuffle_buffer_size, dim, seed, decode_dtype)
+                   shuffle_buffer_size, dim, seed, decode_dtype, shard)
+
+
+def close_iterator(it) -> None:
+    """Release an iterator of a Dataset (prefetch thread or generator)."""
+    close = getattr(it, "close", None)
+    if close is not None:
+        close()

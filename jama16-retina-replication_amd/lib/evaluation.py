@@ -60,6 +60,11 @@ def perform_test(sess, init_op, summary_writer=None, epoch=None,
             return [np.zeros((0, 1), np.float32) for _ in custom_tensors]
         return [np.vstack(x) for x in zip(*batch_results)]
 
+    # data-parallel ranks each ran their own batches: sum the metric states
+    # (no-op for one process) so every rank reads the same Brier / AUC
+    sync = getattr(sess, "sync_metrics", None)
+    if sync is not None:
+        sync("tp", "fp", "fn", "tn", "brier", "auc")
     test_conf_matrix = sess.confusion_matrix()
     test_brier = sess.value("brier")
     test_auc = sess.value("auc")

@@ -68,9 +68,16 @@ def build_parser():
     p.add_argument("--image_size", type=int, default=299, help="input resolution (299; 587 high-res variant)")
     p.add_argument("--num_epochs", type=int, default=NUM_EPOCHS)
     p.add_argument("--seed", type=int, default=0, help="weight init seed (ensemble member index)")
-    p.add_argument("--conv_math", default="x8", choices=["x8", "f32"],
+    p.add_argument("--conv_math", default="x8", choices=["x8", "x8p", "f32"],
                    help="fp32 convolution arithmetic: x8 = exact 3-way bf16 split on the matrix cores (fp32-accurate, "
-                        "default), f32 = fp32 MFMA")
+                        "default), x8p = the same on pre-split operand planes, f32 = fp32 MFMA")
+    p.add_argument("--tiles", default="heuristic", choices=["heuristic", "autotune"],
+                   help="conv tile configs: heuristic (default; a function of the layer shapes only, so two runs on "
+                        "any MI355X sum in the same order and train bitwise-equal) or autotune (timed on rank 0 at "
+                        "start, broadcast to every rank); the table in use is saved in the checkpoint .meta")
+    p.add_argument("--tile_table", default=None,
+                   help="checkpoint path (or JSON file) whose saved tile table to reuse: reproduces that run's "
+                        "summation order exactly")
     p.add_argument("--shuffle_seed", type=int, default=None)
     p.add_argument("--max_steps_per_epoch", type=int, default=None)
     return p
@@ -83,6 +90,20 @@ def status_line(epoch, num_epochs, batch_num, xent, i_step=None):
     if i_step is not None:
         parts.append(f"Step: {i_step:>10}")
     return ", ".join(parts)
+
+
+def load_tile_table(path: str) -> dict:
+    """A saved tile table: from a checkpoint's .meta (jr.checkpoint) or a
+    JSON file holding the table itself."""
+    import json
+    from jr import checkpoint
+    if path.endswith(".json"):
+        with open(path) as f:
+            return json.load(f)
+    meta = checkpoint.read_meta(path)
+    if "tile_table" not in meta:
+        raise ValueError(f"{path}: checkpoint carries no tile table")
+    return meta["tile_table"]
 
 
 def main(argv=None):
@@ -120,57 +141,83 @@ Use SGD: {bool(args.vanilla_sgd)}
     thresholds = lib.metrics.generate_thresholds(NUM_THRESHOLDS, KEPSILON) + [0.5]
     size = [args.image_size, args.image_size]
     shuffle_seed = args.shuffle_seed if args.shuffle_seed is not None else int.from_bytes(os.urandom(4), "little")
-    if dist:   # every rank walks the same shuffled stream and takes its batches
+    if dist:   # every rank walks the same shuffled stream of record handles
         t = torch.tensor([shuffle_seed], dtype=torch.int64, device="cuda")
         dist.broadcast(t, 0)
         shuffle_seed = int(t.item())
+    # data parallel: each rank decodes only its own batches (b % world ==
+    # rank) of the common stream; validation and the final sweep likewise,
+    # with the metric counts summed over ranks (Session.sync_metrics)
+    shard = (rank, world) if dist else None
     train_dataset = lib.dataset.initialize_dataset(
         args.train_dir, TRAIN_BATCH_SIZE, num_workers=NUM_WORKERS,
         prefetch_buffer_size=2 * TRAIN_BATCH_SIZE, shuffle_buffer_size=SHUFFLE_BUFFER_SIZE,
         image_data_format="channels_last", num_channels=NUM_CHANNELS, image_dim=size,
-        seed=shuffle_seed, decode_dtype="uint8")
+        seed=shuffle_seed, decode_dtype="uint8", shard=shard)
     val_dataset = lib.dataset.initialize_dataset(
         args.val_dir, VAL_BATCH_SIZE, num_workers=NUM_WORKERS,
         prefetch_buffer_size=2 * TRAIN_BATCH_SIZE, shuffle_buffer_size=SHUFFLE_BUFFER_SIZE,
         image_data_format="channels_last", num_channels=NUM_CHANNELS, image_dim=size,
-        seed=shuffle_seed + 1, decode_dtype="uint8")
+        seed=shuffle_seed + 1, decode_dtype="uint8", shard=shard)
 
     engine = Engine(max(TRAIN_BATCH_SIZE, VAL_BATCH_SIZE), args.image_size, args.image_size,
                     device=local, optimizer="sgd" if args.vanilla_sgd else ("nesterov" if USE_NESTEROV else "momentum"),
-                    lr=LEARNING_RATE, momentum=MOMENTUM, seed=args.seed, conv_math=args.conv_math)
+                    lr=LEARNING_RATE, momentum=MOMENTUM, seed=args.seed, conv_math=args.conv_math, autotune=False)
+    engine.clear_tile_table()
+    table = None
+    if args.tile_table:
+        table = load_tile_table(args.tile_table)
+    elif args.tiles == "autotune" and rank == 0:
+        engine.autotune()
+        table = engine.tile_table()
+    if dist and args.tiles == "autotune" and not args.tile_table:
+        box = [table]
+        dist.broadcast_object_list(box, 0)
+        table = box[0]
+    if table is not None:
+        engine.set_tile_table(table)
     sess = Session(engine, thresholds, NUM_THRESHOLDS, KEPSILON)
     if dist:
         from jr.dist import BucketAllReduce
         sess.allreduce = BucketAllReduce(engine, world)
-        sess.shard = (rank, world)
+
+        def _sum_over_ranks(vec):
+            t = torch.from_numpy(vec).to("cuda")
+            dist.all_reduce(t)
+            return t.cpu().numpy()
+        sess.reduce = _sum_over_ranks
     train_writer = FileWriter(os.path.join(args.save_summaries_dir, "train")) if rank == 0 else None
 
     latest_peak_auc = 0.0
     waited_epochs = 0
     saved = False
     steps_per_epoch = None
-    if dist:
-        n_batches = -(-train_dataset.num_records() // TRAIN_BATCH_SIZE)
-        steps_per_epoch = n_batches // world
+    if dist:   # every rank runs the same number of steps (matching collectives)
+        steps_per_epoch = -(-train_dataset.num_records() // TRAIN_BATCH_SIZE) // world
     for epoch in range(args.num_epochs):
         sess.reset("brier")
         batch_num = 0
-        for i, (images, labels) in enumerate(train_dataset):
-            if dist and i % world != rank:
-                continue
-            if steps_per_epoch is not None and batch_num >= steps_per_epoch:
-                break
-            if args.max_steps_per_epoch is not None and batch_num >= args.max_steps_per_epoch:
-                break
-            i_global, xent, probs = sess.train_batch(images, labels)
-            sess.update(labels, probs, "brier")
-            if rank == 0:
-                print(status_line(epoch, args.num_epochs, batch_num, xent, i_global), end="\r")
-            batch_num += 1
+        it = iter(train_dataset)
+        try:
+            for images, labels in it:
+                if steps_per_epoch is not None and batch_num >= steps_per_epoch:
+                    break
+                if args.max_steps_per_epoch is not None and batch_num >= args.max_steps_per_epoch:
+                    break
+                i_global, xent, probs = sess.train_batch(images, labels)
+                sess.update(labels, probs, "brier")
+                if rank == 0:
+                    print(status_line(epoch, args.num_epochs, batch_num, xent, i_global), end="\r")
+                batch_num += 1
+        finally:
+            lib.dataset.close_iterator(it)
+        sess.sync_metrics("brier")
         train_brier = sess.value("brier")
         if rank == 0:
             print("\nEnd of epoch {0}! (Brier: {1:8.6})".format(epoch, train_brier))
 
+        # every rank gets the same val_auc (summed counts), so the early-stop
+        # decisions below agree and the collectives stay matched
         val_auc = lib.evaluation.perform_test(sess=sess, init_op=val_dataset,
                                               summary_writer=train_writer, epoch=epoch)
         if val_auc < latest_peak_auc + MIN_DELTA_AUC:
@@ -184,7 +231,7 @@ Use SGD: {bool(args.vanilla_sgd)}
             if rank == 0:
                 print(f"New peak auc reached: {val_auc:10.8}")
                 checkpoint.save(args.save_model_path, engine.g, engine.params_numpy(),
-                                {"epoch": epoch, "val_auc": float(val_auc)})
+                                {"epoch": epoch, "val_auc": float(val_auc), "tile_table": engine.tile_table()})
             saved = True
             waited_epochs = 0
 
@@ -196,9 +243,14 @@ Use SGD: {bool(args.vanilla_sgd)}
         flat, _ = checkpoint.load(args.save_model_path, engine.g)
         engine.load_params(flat)
     sess.reset("tp", "fp", "fn", "tn")
-    for images, labels in train_dataset:
-        probs = sess.predict(images, labels)
-        sess.update(labels, probs, "tp", "fp", "fn", "tn")
+    it = iter(train_dataset)
+    try:
+        for images, labels in it:
+            probs = sess.predict(images, labels)
+            sess.update(labels, probs, "tp", "fp", "fn", "tn")
+    finally:
+        lib.dataset.close_iterator(it)
+    sess.sync_metrics("tp", "fp", "fn", "tn")
     if rank == 0:
         os.makedirs(os.path.dirname(os.path.abspath(args.save_operating_thresholds_path)), exist_ok=True)
         spec, sens = sess.specificities(), sess.sensitivities()

@@ -10,6 +10,14 @@ graph builder, the graph the reference builds at train.py:128-153:
   (train.py:146-153), with BN always in batch-statistics mode (App. C Q1).
 Backward is torch autograd.  Runs in fp64 for goldens and fp32 for the
 CPU baseline timing in bench.py (kind "port").
+
+emulate_bf16=True is an independent bf16 implementation of the same step
+for the bf16 envelope of tests/test_gpu_baseline_sizes.py: it rounds to bf16
+(RNE) where the bf16 GPU path stores bf16 -- the input image, every filter,
+every raw conv output (BN statistics then see the stored values), every BN+ReLU
+output and average-pool output -- and, in the backward, the gradients of those
+stored tensors (custom autograd rounding both ways); arithmetic stays in the
+oracle's dtype (fp64).
 """
 from __future__ import annotations
 
@@ -20,11 +28,24 @@ import torch.nn.functional as F
 EPS = 1e-3
 
 
+class _RoundBF16(torch.autograd.Function):
+    """bf16 storage: round the value forward and its gradient backward."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
 class InceptionV3Ref:
     """Functional Inception-v3 over a {name: tensor} parameter dict (HWIO)."""
 
-    def __init__(self, params: dict, dtype=torch.float64, requires_grad=True):
+    def __init__(self, params: dict, dtype=torch.float64, requires_grad=True, emulate_bf16=False):
         self.dtype = dtype
+        self.bf16 = emulate_bf16
         self.P = {k: torch.tensor(np.asarray(v), dtype=dtype, requires_grad=requires_grad)
                   for k, v in params.items()}
         self._k = 0
@@ -37,29 +58,32 @@ class InceptionV3Ref:
         beta = self.P[f"batch_normalization_{self._k}/beta"]
         assert tuple(w.shape) == (num_row, num_col, x.shape[1], filters), (self._k, tuple(w.shape))
         pad = ((num_row - 1) // 2, (num_col - 1) // 2) if padding == "same" else (0, 0)
-        y = F.conv2d(x, w.permute(3, 2, 0, 1), stride=strides, padding=pad)
+        y = F.conv2d(x, self._r(w).permute(3, 2, 0, 1), stride=strides, padding=pad)
+        y = self._r(y)                                                  # raw output as stored
         mean = y.mean(dim=(0, 2, 3), keepdim=True)
         var = ((y - mean) ** 2).mean(dim=(0, 2, 3), keepdim=True)      # biased
         y = (y - mean) / torch.sqrt(var + EPS) + beta.view(1, -1, 1, 1)
-        y = F.relu(y)
+        y = self._r(F.relu(y))
         if self.record is not None:          # debugging aid: keep every block output
             if y.requires_grad:
                 y.retain_grad()
             self.record.append(y)
         return y
 
+    def _r(self, t):
+        return _RoundBF16.apply(t) if self.bf16 else t
+
     @staticmethod
     def maxpool(x):
         return F.max_pool2d(x, 3, 2)
 
-    @staticmethod
-    def avgpool_same(x):
-        return F.avg_pool2d(x, 3, 1, padding=1, count_include_pad=False)
+    def avgpool_same(self, x):
+        return self._r(F.avg_pool2d(x, 3, 1, padding=1, count_include_pad=False))
 
     def features(self, x_nhwc):
         self._k = 0
         cb = self.conv2d_bn
-        x = x_nhwc.permute(0, 3, 1, 2)
+        x = self._r(x_nhwc.permute(0, 3, 1, 2))
         x = cb(x, 32, 3, 3, strides=(2, 2), padding="valid")
         x = cb(x, 32, 3, 3, padding="valid")
         x = cb(x, 64, 3, 3)

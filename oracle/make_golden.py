@@ -10,7 +10,15 @@ vectors (oracle/__init__.py).  These fixtures freeze the oracle's own outputs
 Weights are NOT stored: they are regenerated from the seed by jr.init
 (numpy PCG64), inputs from jr.synth (PCG64(432 + i)).
 
-  python oracle/make_golden.py [--only ops,metrics,net107,net299,curve]
+  python oracle/make_golden.py [--only ops,metrics,net107,net299,curve,net299b64,net587b2]
+
+BASELINE-size fixtures (net299b64: configs 2-3 geometry, 299^2 B=64;
+net587b2: config 5 geometry, 587^2 B=2) hold the fp64 results AND the same
+step by the fp32 CPU restatement ("*_fp32" keys): the fp32-vs-fp64 gap of an
+independent fp32 implementation is the envelope the GPU tests scale.  Per
+gradient tensor they keep its norm and its projection on a seeded
+Rademacher vector (grad_proj, seed 1000 + index in grad_names): a norm
+misses a permuted or sign-flipped gradient, the projection does not.
 """
 from __future__ import annotations
 
@@ -95,7 +103,13 @@ def metrics():
                         confusion=MR.confusion_matrix(tp[-1], fp[-1], fn[-1], tn[-1]))
 
 
-def _net(res, batch, seed, steps=1, cycle=None, dtype="float64"):
+def grad_projection(g, i):
+    """<g, r_i> for the seeded Rademacher vector r_i (seed 1000 + i)."""
+    r = np.random.default_rng(1000 + i).integers(0, 2, g.size, dtype=np.int8).astype(np.float64) * 2 - 1
+    return float(np.dot(np.asarray(g, np.float64).ravel(), r))
+
+
+def _net(res, batch, seed, steps=1, cycle=None, dtype="float64", proj=False, bf16=False):
     import torch
     from jr import synth
     from jr.inception import build_inception_v3
@@ -103,7 +117,7 @@ def _net(res, batch, seed, steps=1, cycle=None, dtype="float64"):
     from oracle.inception_ref import InceptionV3Ref
     torch.set_num_threads(os.cpu_count() or 8)
     g = build_inception_v3(res, res)
-    ref = InceptionV3Ref(unflatten(g, init_params(g, seed)), getattr(torch, dtype))
+    ref = InceptionV3Ref(unflatten(g, init_params(g, seed)), getattr(torch, dtype), emulate_bf16=bf16)
     pool = cycle or batch
     imgs = synth.fundus_batch(0, pool, res)
     labels = synth.labels(0, pool)
@@ -122,6 +136,9 @@ def _net(res, batch, seed, steps=1, cycle=None, dtype="float64"):
             names = sorted(grads)
             out["grad_names"] = np.array(names)
             out["grad_norms"] = np.array([np.linalg.norm(grads[k_]) for k_ in names])
+            if proj:
+                out["grad_proj"] = np.array([grad_projection(grads[k_], i) for i, k_ in enumerate(names)])
+            del grads
     out["losses"] = np.array(losses)
     out.update(res=np.array(res), batch=np.array(batch), seed=np.array(seed), pool=np.array(pool))
     return out
@@ -150,6 +167,24 @@ def main():
         curve = _net(299, 4, 0, steps=100, cycle=8)
         curve["losses_fp32_cpu"] = _net(299, 4, 0, steps=100, cycle=8, dtype="float32")["losses"]
         np.savez_compressed(os.path.join(OUT, "loss_curve_res299_b4.npz"), **curve)
+    if "curve16" in todo:
+        # 100 Nesterov steps at B=16, 299^2, fixed unshuffled stream of 32
+        # images (two alternating batches), fp64 and fp32 CPU: per-step
+        # tracking fixture (BN populations 16x larger than the B=4 curve)
+        curve = _net(299, 16, 0, steps=100, cycle=32)
+        curve["losses_fp32_cpu"] = _net(299, 16, 0, steps=100, cycle=32, dtype="float32")["losses"]
+        np.savez_compressed(os.path.join(OUT, "loss_curve_res299_b16.npz"), **curve)
+        print(f"curve16: {time.time() - t0:.0f}s", flush=True)
+    for key, res, batch in (("net299b64", 299, 64), ("net587b2", 587, 2)):
+        if key in todo:
+            d = _net(res, batch, 0, proj=True)
+            d32 = _net(res, batch, 0, dtype="float32", proj=True)
+            dbf = _net(res, batch, 0, proj=True, bf16=True)
+            for k_ in ("logits", "probs", "loss0", "grad_norms", "grad_proj"):
+                d[k_ + "_fp32"] = d32[k_]
+                d[k_ + "_bf16emu"] = dbf[k_]
+            np.savez_compressed(os.path.join(OUT, f"net_res{res}_b{batch}.npz"), **d)
+            print(f"{key}: {time.time() - t0:.0f}s", flush=True)
     print(f"golden fixtures written to {OUT} in {time.time() - t0:.0f}s")
 
 

@@ -48,8 +48,15 @@ def test_validation_errors_without_gpu():
     assert L.jr_conv2d_num_configs(2) == L.jr_conv2d_num_configs(0) > 0
     for op in range(3):
         assert L.jr_conv2d_workspace_size(ctypes.byref(d), op, 2) == L.jr_conv2d_workspace_size(ctypes.byref(d), op, 0)
-    assert L.jr_conv2d_num_configs(3) == 0
-    assert L.jr_conv2d_fwd(ctypes.byref(d), 3, 16, 16, 16, None, 0, None) == -1      # bad dtype
+    # JR_F32_X8P (dtype 3): bf16-operand channel rules (radix 8), its own tile table
+    assert L.jr_conv2d_num_configs(3) > 0
+    assert L.jr_conv2d_workspace_size(ctypes.byref(d), 0, 3) > 0
+    d4 = _ffi.ConvDesc(2, 17, 17, 68, 96, 3, 3, 1, 1, 1, 1, 17, 17, 0, 68, 0, 96)
+    assert L.jr_conv2d_fwd(ctypes.byref(d4), 3, 16, 16, 16, None, 0, None) == -1     # strides % 8
+    assert L.jr_conv2d_num_configs(4) == 0
+    assert L.jr_conv2d_fwd(ctypes.byref(d), 4, 16, 16, 16, None, 0, None) == -1      # bad dtype
+    assert L.jr_split_x8p(16, 10, 6, 0, 4, 16, 8, 0, 8, 80, None) == -1              # slice past src stride
+    assert L.jr_split_x8p(16, 10, 4, 0, 4, 16, 8, 0, 8, 40, None) == -1              # planes overlap
     assert L.jr_bn_relu_apply(2, 16, 0, 8, 10, 8, 16, 16, 16, 16, 0, 8, None) == -1   # x8 is conv-only
     assert L.jr_bn_relu_apply(0, 16, 0, 6, 10, 6, 16, 16, 16, 16, 0, 6, None) == -1   # c % 4
     assert L.jr_bn_relu_apply(0, 16, 4, 8, 10, 8, 16, 16, 16, 16, 0, 8, None) == -1   # x slice out of range

@@ -70,3 +70,18 @@ def test_summary_writer_writes_tfrecord_events(tmp_path):
     w.close()
     recs = list(tfrecord.read_records(w.path))
     assert len(recs) == 2 and b"brain.Event:2" in recs[0] and b"auc" in recs[1]
+
+
+def test_glob_ignores_incomplete_checkpoints(tmp_path):
+    """A leftover `.data-*.tmp` of an interrupted save strips to
+    `<path>.data-00000-of-00001`, which is not a checkpoint: dropped."""
+    import evaluate
+    from jr import checkpoint
+    from jr.inception import build_inception_v3
+    from jr.init import init_params
+    g = build_inception_v3(75, 75)
+    checkpoint.save(str(tmp_path / "model_1"), g, init_params(g, 1))
+    open(str(tmp_path / "model_2") + checkpoint.DATA_SUFFIX + ".tmp", "wb").write(b"partial")
+    assert evaluate.expand_model_paths(str(tmp_path / "model_*")) == [str(tmp_path / "model_1")]
+    meta = checkpoint.read_meta(str(tmp_path / "model_1"))
+    assert (meta["height"], meta["width"]) == (75, 75)

@@ -236,3 +236,63 @@ def test_damaged_file_delivers_records_before_the_damage(tmp_path):
         for x, _ in D.initialize_dataset(d, 2, image_dim=[32, 32]):
             got.append(len(x))
     assert got == [2, 2, 2]                           # records 0-5, then DataLoss at record 6
+
+
+def test_shards_partition_the_stream_and_decode_only_their_batches(records, monkeypatch):
+    """shard=(rank, world): the ranks' batches are exactly the single-process
+    batches b % world == rank, in order, over several seeded-shuffle epochs,
+    and each rank decodes only its own batches (JPEG work split, not
+    repeated)."""
+    import lib.dataset as D
+    calls = []
+    real = D.decode_jpeg
+    monkeypatch.setattr(D, "decode_jpeg", lambda data: (calls.append(1), real(data))[1])
+    kw = dict(image_dim=[64, 64], shuffle_buffer_size=16, seed=9, decode_dtype="uint8")
+    full = D.initialize_dataset(records, 4, **kw)
+    ref = [list(full) for _ in range(2)]                       # two epochs
+    world = 3
+    for rank in range(world):
+        ds = D.initialize_dataset(records, 4, shard=(rank, world), **kw)
+        for epoch in range(2):
+            calls.clear()
+            got = list(ds)
+            want = ref[epoch][rank::world]
+            assert len(got) == len(want)
+            for (x, y), (wx, wy) in zip(got, want):
+                np.testing.assert_array_equal(x, wx)
+                np.testing.assert_array_equal(y, wy)
+            assert len(calls) == sum(len(b[0]) for b in want)  # own batches only
+    with pytest.raises(ValueError):
+        D.initialize_dataset(records, 4, shard=(2, 2))
+
+
+def test_seeded_epochs_agree_after_an_early_stop(records):
+    """A rank that stops an epoch early (capped steps) still shuffles the
+    next epoch like the others: epoch k's order depends on (seed, k) only."""
+    import lib.dataset as D
+    kw = dict(image_dim=[64, 64], shuffle_buffer_size=16, seed=4, decode_dtype="uint8")
+    a, b = D.initialize_dataset(records, 4, **kw), D.initialize_dataset(records, 4, **kw)
+    it = iter(a)
+    next(it)                                                  # epoch 0 cut short
+    D.close_iterator(it)
+    list(b)                                                   # epoch 0 in full
+    for (x, _), (y, _) in zip(a, b):                          # epoch 1
+        np.testing.assert_array_equal(x, y)
+
+
+def test_prefetch_close_stops_the_pipeline(records):
+    """close() after an early break ends the prefetch thread and shuts the
+    decode pool down (no per-epoch thread leak)."""
+    import threading
+    import lib.dataset as D
+    ds = D.initialize_dataset(records, 2, image_dim=[64, 64], prefetch_buffer_size=4)
+    before = threading.active_count()
+    for _ in range(3):
+        it = iter(ds)
+        next(it)
+        D.close_iterator(it)
+        it.join(timeout=10)
+        assert not it._t.is_alive()
+        with pytest.raises(StopIteration):
+            next(it)
+    assert threading.active_count() <= before + 1
