@@ -33,10 +33,12 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 # MI355X dense MFMA (MI355X_MICROARCH.md); x8 = eight bf16 MFMAs per fp32 product
-PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0, "x8": round(2500.0 / 8, 1)}
+PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0, "x8": round(2500.0 / 8, 1), "x8p": round(2500.0 / 8, 1)}
 CONV_MATH = {"f32": "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
              "x8": "fp32 via exact 3-way bf16 split, 8 bf16 MFMAs per product (all terms > 2^-32), "
-                   "fp32 accumulate (JR_F32_X8)"}
+                   "fp32 accumulate (JR_F32_X8)",
+             "x8p": "fp32 via exact 3-way bf16 split done once per operand (jr_split_x8p planes), 8 bf16 MFMAs "
+                    "per product, fp32 accumulate (JR_F32_X8P)"}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -51,7 +53,7 @@ def parse():
                          "evaluate.py:166-211 (BASELINE config 4)")
     ap.add_argument("--res", type=int, default=299)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
-    ap.add_argument("--conv-math", default="x8", choices=["f32", "x8"],
+    ap.add_argument("--conv-math", default="x8", choices=["f32", "x8", "x8p"],
                     help="dtype f32 only. x8 (default): fp32 tensors, products from an exact 3-way bf16 split "
                          "(jr.h JR_F32_X8, fp32-accurate); f32: fp32 MFMA")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a HIP graph")
@@ -224,7 +226,7 @@ def main():
         if not args.no_roofline:
             flops, tconv, nconv = conv_roofline(eng)
             ach = flops / tconv / 1e12
-            peak = PEAK_TFLOPS["x8" if math == "x8" else args.dtype]
+            peak = PEAK_TFLOPS[math if math in ("x8", "x8p") else args.dtype]
             roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": None,
                     "kernel": f"conv implicit-GEMM {'fwd+dgrad+wgrad' if train else 'fwd'} ({nconv} calls/step)",

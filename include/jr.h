@@ -273,6 +273,26 @@ int jr_example_parse_image(const uint8_t* base, const uint64_t* offsets, const u
                            uint64_t* enc_off, uint64_t* enc_len, int64_t* label, int64_t* height,
                            int64_t* width, int32_t* status);
 
+/* ---- collectives: data-parallel gradient exchange over RCCL / xGMI ----
+ * Replaces the reference's only multi-GPU path, the external
+ * tf_cnn_benchmarks parameter server (benchmarks.yaml.jinja.example:81-90;
+ * SURVEY.md §2 row 14, §8b/§8e): one communicator per process (one process
+ * per GPU), in-place sum of the flat gradient enqueued on the caller's
+ * stream.  The 128-byte unique id comes from rank 0's jr_comm_unique_id and
+ * reaches the other ranks through the caller's bootstrap, or through a file
+ * (jr_comm_init_file: rank 0 writes it with an atomic rename, the others
+ * poll up to timeout_ms, < 0 = forever). */
+#define JR_COMM_ID_BYTES 128
+typedef struct jr_comm jr_comm;
+int jr_comm_unique_id(uint8_t* id);
+int jr_comm_init(int rank, int world, const uint8_t* id, int device, jr_comm** comm);
+int jr_comm_init_file(int rank, int world, const char* uid_path, int device, int timeout_ms, jr_comm** comm);
+/* buf[0..n) = sum over the ranks of buf[0..n), dtype JR_F32 or JR_BF16 */
+int jr_allreduce_sum(jr_comm* comm, void* buf, size_t n, int dtype, void* stream);
+int jr_comm_rank(const jr_comm* comm);
+int jr_comm_world(const jr_comm* comm);
+int jr_comm_destroy(jr_comm* comm);
+
 /* ---- HIP graph capture of a whole step ------------------------------ */
 int jr_graph_begin(void* stream);
 int jr_graph_end(void* stream, void** graph_exec);

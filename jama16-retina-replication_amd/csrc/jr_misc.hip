@@ -3,8 +3,12 @@
 // Optimizers replace the TF ApplyMomentum / ApplyGradientDescent ops that
 // .minimize adds at train.py:147-153.  One launch updates
 // the whole flat parameter buffer (21,770,401 fp32 values); each lane moves
-// 16-byte vectors and the arithmetic is written with explicit _rn intrinsics
-// so it is the unfused TF expression order:
+// 16-byte vectors and the arithmetic is the unfused TF expression order.
+// NOTE: hipcc contracts a*b+c into an FMA by default (-ffp-contract=fast),
+// and without OCML_BASIC_ROUNDED_OPERATIONS __fmul_rn / __fadd_rn are the
+// plain operators, so this file is compiled with -ffp-contract=off
+// (Makefile): every multiply and add rounds on its own,
+// the IEEE fp32 evaluation of TF's (Eigen, non-fused) expressions:
 //   ApplyMomentum(use_nesterov): accum = accum*m + g; var -= g*lr + accum*m*lr
 //   ApplyMomentum:               accum = accum*m + g; var -= accum*lr
 //   ApplyGradientDescent:        var -= g*lr
@@ -63,18 +67,38 @@ __global__ void __launch_bounds__(256) k_sgd(float* __restrict__ w, const float*
     w[i] = __fsub_rn(w[i], __fmul_rn(__fmul_rn(grad[i], gs), lr));
 }
 
-// TF ApplyAdam: m = m + (g - m)(1-b1); v = v + (g^2 - v)(1-b2);
-// var -= lr_t * m / (sqrt(v) + eps)   with lr_t = lr*sqrt(1-b2^t)/(1-b1^t) from the host.
+// Correctly rounded sqrt (IEEE, as Eigen's sqrt on the CPU): v_sqrt_f32 is
+// within 1 ulp, so check its neighbours with exact fma residuals and step
+// once (denormal inputs are scaled by 2^32 first).
+__device__ __forceinline__ float sqrt_cr(float x) {
+  const bool tiny = x < 0x1.0p-96f;
+  const float xs = tiny ? x * 0x1.0p+32f : x;
+  float s = __builtin_amdgcn_sqrtf(xs);
+  const float dn = __uint_as_float(__float_as_uint(s) - 1), up = __uint_as_float(__float_as_uint(s) + 1);
+  if (__builtin_fmaf(-dn, s, xs) <= 0.f) s = dn;
+  else if (__builtin_fmaf(-up, s, xs) > 0.f) s = up;
+  s = tiny ? s * 0x1.0p-16f : s;
+  return (xs == 0.f || !(xs < __builtin_inff())) ? __builtin_sqrtf(x) : s;
+}
+
+// TF ApplyAdam (training_ops.cc ApplyAdamNonCuda, Eigen, no contraction):
+//   m += (g - m) * (1 - beta1);  v += (g*g - v) * (1 - beta2);
+//   var -= (m * alpha) / (sqrt(v) + epsilon),
+//   alpha = lr * sqrt(1 - beta2^t) / (1 - beta1^t) (lr_t, computed on the host);
+// every operation a correctly rounded _rn intrinsic in that order, so the
+// update is bitwise the IEEE fp32 evaluation of TF's expression.
 __global__ void __launch_bounds__(256) k_adam(float* __restrict__ w, const float* __restrict__ grad,
                                               float* __restrict__ mm, float* __restrict__ vv, int64_t n,
                                               float lr_t, float b1, float b2, float eps, float gs) {
+  const float one_b1 = __fsub_rn(1.f, b1), one_b2 = __fsub_rn(1.f, b2);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float g = grad[i] * gs;
-    const float m1 = mm[i] + (g - mm[i]) * (1.f - b1);
-    const float v1 = vv[i] + (g * g - vv[i]) * (1.f - b2);
+    const float g = __fmul_rn(grad[i], gs);
+    const float m0 = mm[i], v0 = vv[i];
+    const float m1 = __fadd_rn(m0, __fmul_rn(__fsub_rn(g, m0), one_b1));
+    const float v1 = __fadd_rn(v0, __fmul_rn(__fsub_rn(__fmul_rn(g, g), v0), one_b2));
     mm[i] = m1;
     vv[i] = v1;
-    w[i] -= lr_t * m1 / (sqrtf(v1) + eps);
+    w[i] = __fsub_rn(w[i], __fdiv_rn(__fmul_rn(m1, lr_t), __fadd_rn(sqrt_cr(v1), eps)));
   }
 }
 

@@ -79,6 +79,13 @@ _SIGS = {
                                           c_void_p]),
     "jr_split_x8p": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_int32, c_int32, c_int32,
                              c_int64, c_void_p]),
+    "jr_comm_unique_id": (c_int, [c_void_p]),
+    "jr_comm_init": (c_int, [c_int, c_int, c_void_p, c_int, c_void_p]),
+    "jr_comm_init_file": (c_int, [c_int, c_int, c_char_p, c_int, c_int, c_void_p]),
+    "jr_allreduce_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    "jr_comm_rank": (c_int, [c_void_p]),
+    "jr_comm_world": (c_int, [c_void_p]),
+    "jr_comm_destroy": (c_int, [c_void_p]),
     "jr_bn_workspace_size": (c_size_t, [c_int64, c_int32]),
     "jr_bn_stats": (c_int, [c_int, c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
                             c_void_p, c_size_t, c_void_p]),

@@ -18,14 +18,27 @@ for every bucket before the optimizer.  The mean (1/world) is folded into
 the optimizer launch as grad_scale.  Weights stay bitwise identical across
 ranks because every rank applies the same update to the same reduced
 gradient.
+
+Two transports, same bucket walk:
+  * torch.distributed all_reduce (backend 'nccl' = RCCL; 'gloo' on CPU);
+  * libjr's own RCCL communicator (JrComm: jr_comm_init / jr_allreduce_sum,
+    include/jr.h) on a dedicated comm stream that waits for the engine
+    stream at each bucket's issue point; the engine stream waits for the
+    comm stream before the optimizer.
+and two payloads: fp32 (default; the sum of fp32 gradients) or bf16 (43.5 MB
+instead of 87.1 MB: each bucket cast to bf16, summed in bf16 by RCCL, cast
+back; ranks stay identical, the sum carries bf16 rounding).
 """
 from __future__ import annotations
 
 import contextlib
-from typing import List, Tuple
+import ctypes
+from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
+
+from . import _ffi
 
 DEFAULT_BUCKET_BYTES = 24 << 20
 
@@ -49,16 +62,74 @@ def make_buckets(layout, total: int, bucket_bytes: int = DEFAULT_BUCKET_BYTES) -
     return buckets
 
 
+class JrComm:
+    """libjr's RCCL communicator (one per process / GPU)."""
+
+    def __init__(self, rank: int, world: int, device: int, uid: Optional[bytes] = None,
+                 uid_path: Optional[str] = None, timeout_ms: int = 120000):
+        self.lib = _ffi.load()
+        self.h = ctypes.c_void_p()
+        if uid_path is not None:
+            _ffi.check("jr_comm_init_file", self.lib.jr_comm_init_file(rank, world, uid_path.encode(), device,
+                                                                        timeout_ms, ctypes.byref(self.h)))
+        else:
+            if uid is None or len(uid) != 128:
+                raise ValueError("JrComm needs the 128-byte unique id of rank 0 (JrComm.unique_id())")
+            buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+            _ffi.check("jr_comm_init", self.lib.jr_comm_init(rank, world, buf, device, ctypes.byref(self.h)))
+        self.rank, self.world = rank, world
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        _ffi.check("jr_comm_unique_id", _ffi.load().jr_comm_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def from_torch_group(cls, rank: int, world: int, device: int) -> "JrComm":
+        """Bootstrap the id through an initialised torch.distributed group."""
+        box = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, 0)
+        return cls(rank, world, device, uid=box[0])
+
+    def allreduce(self, ptr: int, n: int, dtype: int, stream) -> None:
+        _ffi.check("jr_allreduce_sum", self.lib.jr_allreduce_sum(self.h, ctypes.c_void_p(ptr), n, dtype,
+                                                                  ctypes.c_void_p(stream)))
+
+    def close(self) -> None:
+        if self.h:
+            _ffi.check("jr_comm_destroy", self.lib.jr_comm_destroy(self.h))
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class BucketAllReduce:
     """Per-step state machine: begin() -> param_ready(offset)* -> finish()."""
 
-    def __init__(self, engine, world: int, bucket_bytes: int = DEFAULT_BUCKET_BYTES, group=None):
+    def __init__(self, engine, world: int, bucket_bytes: int = DEFAULT_BUCKET_BYTES, group=None,
+                 comm: Optional[JrComm] = None, payload: str = "f32"):
+        if payload not in ("f32", "bf16"):
+            raise ValueError("payload must be 'f32' or 'bf16'")
         self.eng = engine
         self.world = world
         self.group = group
+        self.comm = comm
+        self.payload = payload
         self.buckets = make_buckets(engine.layout, engine.nparam, bucket_bytes)
         self.works = []
         self.next = 0
+        dev = getattr(engine, "device", None)
+        self.half = (torch.empty(engine.nparam, dtype=torch.bfloat16, device=dev or engine.grads.device)
+                     if payload == "bf16" else None)
+        if comm is not None:
+            self.comm_stream = torch.cuda.Stream(device=engine.grads.device)
+            self._ready_ev = torch.cuda.Event()
+            self._done_ev = torch.cuda.Event()
 
     def begin(self, eng=None) -> None:
         self.works = []
@@ -68,13 +139,41 @@ class BucketAllReduce:
         s = getattr(self.eng, "stream", None)
         return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
 
-    def _issue_ready(self, ready_from: int) -> None:
+    def _cast(self, fn, src: int, dst: int, n: int, stream) -> None:
+        _ffi.check(fn, getattr(_ffi.load(), fn)(ctypes.c_void_p(src), ctypes.c_void_p(dst), n,
+                                                ctypes.c_void_p(stream)))
+
+    def _issue_jr(self, lo: int, hi: int) -> None:
+        eng, cs = self.eng, self.comm_stream
+        self._ready_ev.record(eng.stream)           # the bucket's gradients are final on the engine stream
+        cs.wait_event(self._ready_ev)
+        g = eng.grads.data_ptr() + 4 * lo
+        if self.half is None:
+            self.comm.allreduce(g, hi - lo, _ffi.JR_F32, cs.cuda_stream)
+        else:
+            h = self.half.data_ptr() + 2 * lo
+            self._cast("jr_cast_f32_to_bf16", g, h, hi - lo, cs.cuda_stream)
+            self.comm.allreduce(h, hi - lo, _ffi.JR_BF16, cs.cuda_stream)
+            self._cast("jr_cast_bf16_to_f32", h, g, hi - lo, cs.cuda_stream)
+
+    def _issue_torch(self, lo: int, hi: int):
         eng = self.eng
+        with self._stream_ctx():
+            if self.half is None:
+                return dist.all_reduce(eng.grads[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            st = eng.stream.cuda_stream if getattr(eng, "stream", None) is not None else 0
+            self._cast("jr_cast_f32_to_bf16", eng.grads.data_ptr() + 4 * lo, self.half.data_ptr() + 2 * lo,
+                       hi - lo, st)
+            w = dist.all_reduce(self.half[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            return (w, lo, hi)
+
+    def _issue_ready(self, ready_from: int) -> None:
         while self.next < len(self.buckets) and self.buckets[self.next][0] >= ready_from:
             lo, hi = self.buckets[self.next]
-            with self._stream_ctx():
-                w = dist.all_reduce(eng.grads[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            self.works.append(w)
+            if self.comm is not None:
+                self._issue_jr(lo, hi)
+            else:
+                self.works.append(self._issue_torch(lo, hi))
             self.next += 1
 
     def param_ready(self, offset: int) -> None:
@@ -84,8 +183,19 @@ class BucketAllReduce:
 
     def finish(self, eng=None) -> float:
         self._issue_ready(0)
+        if self.comm is not None:
+            self._done_ev.record(self.comm_stream)
+            self.eng.stream.wait_event(self._done_ev)
+            return 1.0 / self.world
         with self._stream_ctx():
             for w in self.works:
-                w.wait()
+                if isinstance(w, tuple):
+                    w, lo, hi = w
+                    w.wait()
+                    st = self.eng.stream.cuda_stream if getattr(self.eng, "stream", None) is not None else 0
+                    self._cast("jr_cast_bf16_to_f32", self.half.data_ptr() + 2 * lo,
+                               self.eng.grads.data_ptr() + 4 * lo, hi - lo, st)
+                else:
+                    w.wait()
         self.works = []
         return 1.0 / self.world

@@ -71,9 +71,13 @@ class Engine:
         self.x8p = conv_math == "x8p"
         self.cdt = {"x8": _ffi.JR_F32_X8, "x8p": _ffi.JR_F32_X8P}.get(conv_math, self.dt)
         self.train_mode = train
+        if optimizer not in ("nesterov", "momentum", "sgd", "adam"):
+            raise ValueError(f"unknown optimizer {optimizer}")
         self.optimizer = optimizer
         self.lr = float(lr)
         self.momentum = float(momentum)
+        # Adam (north-star extra; TF AdamOptimizer defaults): accum holds m
+        self.adam_b1, self.adam_b2, self.adam_eps, self.adam_t = 0.9, 0.999, 1e-8, 0
         self.head_mode = _ffi.JR_HEAD_SIGMOID if head == "sigmoid" else _ffi.JR_HEAD_SOFTMAX
         self.units = self.g.units
         self.stream = torch.cuda.Stream(device=self.device)
@@ -144,6 +148,7 @@ class Engine:
         if self.train_mode:
             self.grads = self._t(self.nparam)
             self.accum = self._t(self.nparam)
+            self.adam_v = self._t(self.nparam) if self.optimizer == "adam" else None
             self.dacts = [self._t(B * b.h * b.w * b.c, at) if b.id != g.input_buf else None
                           for b in g.bufs]
             # per-lane scratch for the raw-output gradient of the launch in flight
@@ -520,8 +525,10 @@ class Engine:
                                                 self.momentum, 1.0, s0), "momentum", 0, greads, [("p",), ("acc",)])
             elif self.optimizer == "sgd":
                 add(opt, L.jr_sgd_update, (P, G, self.nparam, self.lr, 1.0, s0), "sgd", 0, greads, [("p",)])
-            else:
-                raise ValueError(f"unknown optimizer {self.optimizer}")
+            else:   # adam: lr_t of the step is filled in by apply_update
+                add(opt, L.jr_adam_update, (P, G, self.accum.data_ptr(), self.adam_v.data_ptr(), self.nparam,
+                                            self.lr, self.adam_b1, self.adam_b2, self.adam_eps, 1.0, s0),
+                    "adam", 0, greads, [("p",), ("acc",)])
         schedule(seq)
         self._calls[key] = (fwd, bwd, opt, keep, None)
         return self._calls[key]
@@ -599,10 +606,16 @@ class Engine:
 
     def apply_update(self, B: Optional[int] = None, grad_scale: float = 1.0) -> None:
         _, _, opt, _, ev = self._build_calls(B or self.batch)
-        if grad_scale != 1.0:
+        if grad_scale != 1.0 or self.optimizer == "adam":
             c = opt[0]
             args = list(c.args)
             args[-2] = grad_scale
+            if self.optimizer == "adam":
+                # TF ApplyAdam's alpha = lr sqrt(1 - b2^t) / (1 - b1^t), host fp64
+                # (so Adam steps run eagerly: the scalar changes every step)
+                self.adam_t += 1
+                t = self.adam_t
+                args[5] = self.lr * (1.0 - self.adam_b2 ** t) ** 0.5 / (1.0 - self.adam_b1 ** t)
             opt = [dataclasses.replace(c, args=tuple(args))]
         self._run(opt, ev)
 
@@ -622,13 +635,16 @@ class Engine:
         self.apply_update(B, grad_scale=scale)
 
     def capture(self, B: Optional[int] = None) -> None:
-        """Capture fwd+bwd+update for batch B into a HIP graph (single GPU);
+        """Capture fwd+bwd+update for batch B into a HIP graph (single GPU;
+        not for Adam, whose step scalar changes every step);
         the lanes become parallel branches of the graph.  Up to two lanes
         the lane streams themselves are captured (fork/join by events: the
         faster graph on ROCm 7.2); beyond that the DAG is built explicitly
         on ONE capturing stream (capture_dag), because cross-waits among
         three or more captured streams crashed hipGraphInstantiate."""
         B = B or self.batch
+        if self.optimizer == "adam":
+            raise ValueError("Adam steps run eagerly (the step's alpha is a host scalar)")
         if self.nlanes > 2:
             return self.capture_dag(B)
         fwd, bwd, opt, _, _ = self._build_calls(B)

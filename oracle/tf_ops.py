@@ -197,3 +197,40 @@ def nesterov(w, g, a, lr=3e-3, m=0.9):
 def sgd(w, g, lr=3e-3):
     """GradientDescentOptimizer at train.py:147-148."""
     return w - lr * g
+
+
+def momentum(w, g, a, lr=3e-3, m=0.9):
+    """MomentumOptimizer(use_nesterov=False) (the -sgd-less, Nesterov-less
+    form of train.py:150-153) -> TF ApplyMomentum: accum = accum*m + g;
+    var -= accum*lr."""
+    a = a * m + g
+    return w - a * lr, a
+
+
+def adam_f32(w, g, m, v, t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8):
+    """TF AdamOptimizer -> ApplyAdam (north-star extra; not used by the
+    reference), restated in IEEE fp32 in TF's operation order (Eigen, no
+    fused multiply-add): m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2);
+    var -= (m * alpha) / (sqrt(v) + eps), alpha = lr sqrt(1 - b2^t) / (1 - b1^t)
+    (computed in fp64 then rounded, as the host passes it).  Returns
+    (w, m, v, alpha) as float32."""
+    f = np.float32
+    w, g, m, v = (np.asarray(a, np.float32) for a in (w, g, m, v))
+    alpha = f(lr * np.sqrt(1 - b2 ** t) / (1 - b1 ** t))
+    one_b1, one_b2 = f(1) - f(b1), f(1) - f(b2)
+    m = m + (g - m) * one_b1
+    v = v + (g * g - v) * one_b2
+    w = w - (m * alpha) / (np.sqrt(v) + f(eps))
+    return w, m, v, alpha
+
+
+def softmax_xent_mean(z, y):
+    """Softmax-head mode (north-star extra): mean over samples of
+    -sum_u y log softmax(z)_u; returns (loss, probs, dz)."""
+    z = np.asarray(z, np.float64)
+    y = np.asarray(y, np.float64)
+    zm = z - z.max(axis=1, keepdims=True)
+    p = np.exp(zm) / np.exp(zm).sum(axis=1, keepdims=True)
+    lse = np.log(np.exp(zm).sum(axis=1, keepdims=True))
+    loss = float(np.mean(np.sum(y * (lse - zm), axis=1)))
+    return loss, p, (p - y) / z.shape[0]
