@@ -97,6 +97,56 @@ def conv_roofline(eng, steps: int = 3):
     return flops, t, len(pairs) // steps
 
 
+FAMILY = {"bn_relu": "bn_relu_apply", "bn_relu_bwd": "bn_relu_bwd", "maxpool_fwd": "pool_fwd",
+          "avgpool_fwd": "pool_fwd", "maxpool_bwd": "pool_bwd", "avgpool_bwd": "pool_bwd", "nesterov": "optimizer",
+          "split_x8p": "split_x8p"}
+
+
+def family_rates(eng, reps: int = 5) -> dict:
+    """Achieved HBM rates of the bandwidth-bound kernel families over one
+    step: every call of a family (BN+ReLU apply, BN+ReLU backward, pools
+    fwd/bwd, the Nesterov update; x8p's operand splits) captured into ONE HIP
+    graph on the engine stream and replayed back to back, timed with HIP
+    events on that stream; algorithmic bytes = each call's declared reads +
+    writes (jr.engine: e.g. BN apply 2 x M x C x elem, BN backward 3 passes,
+    Nesterov 20 B/param).  Run after the timed region (the replays rewrite
+    activations / scratch the next real step recomputes)."""
+    from collections import defaultdict
+    from jr import _ffi
+    L = eng.lib
+    fwd, bwd, opt, _, _ = eng._build_calls(eng.batch, 1)
+    fam = defaultdict(list)
+    for c in fwd + bwd + opt:
+        if c.fn != "param_ready" and c.nbytes and c.name in FAMILY:
+            fam[FAMILY[c.name]].append(c)
+    out = {}
+    for name, calls in fam.items():
+        eng.synchronize()
+        _ffi.check("jr_graph_begin", L.jr_graph_begin(eng._s))
+        try:
+            for c in calls:
+                rc = c.fn(*c.args)
+                if rc:
+                    raise _ffi.JRError(c.name, rc, _ffi.last_error())
+        finally:
+            ex = __import__("ctypes").c_void_p()
+            _ffi.check("jr_graph_end", L.jr_graph_end(eng._s, __import__("ctypes").byref(ex)))
+        _ffi.check("jr_graph_launch", L.jr_graph_launch(ex, eng._s))     # warm-up
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(eng.stream)
+        for _ in range(reps):
+            _ffi.check("jr_graph_launch", L.jr_graph_launch(ex, eng._s))
+        e1.record(eng.stream)
+        eng.synchronize()
+        L.jr_graph_destroy(ex)
+        t = e0.elapsed_time(e1) / 1e3 / reps
+        nbytes = sum(c.nbytes for c in calls)
+        gbs = nbytes / t / 1e9
+        out[name] = {"launches": len(calls), "ms_per_step": round(t * 1e3, 3), "bytes_per_step": nbytes,
+                     "achieved_GBs": round(gbs, 1), "frac_of_8TBs": round(gbs / HBM_PEAK_GBS, 3)}
+    return out
+
+
 def pmc_traffic(dtype: str, B: int, res: int, math: str = "x8") -> dict:
     """HBM bytes of the conv family per training step from the committed
     rocprofv3 PMC summary of the same workload (tools/pmc_step.sh ->
@@ -107,9 +157,12 @@ def pmc_traffic(dtype: str, B: int, res: int, math: str = "x8") -> dict:
     cannot run the profiler itself, so `traffic` is null without that file."""
     if (B, res) != (64, 299):
         return {}
-    tag = "f32mfma" if (dtype == "f32" and math == "f32") else dtype
-    p = os.path.join(ROOT, "profiles", f"r01_pmc_{tag}.json")
-    if not os.path.exists(p):
+    tag = {"f32": "f32mfma", "x8p": "f32x8p"}.get(math, "f32") if dtype == "f32" else dtype
+    for rnd in ("r02", "r01"):      # the newest committed summary of this workload
+        p = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{tag}.json")
+        if os.path.exists(p):
+            break
+    else:
         return {}
     fam = json.load(open(p))["families"].get("conv", {})
     if "hbm_read_bytes" not in fam or "hbm_write_bytes" not in fam:
@@ -118,12 +171,36 @@ def pmc_traffic(dtype: str, B: int, res: int, math: str = "x8") -> dict:
             "traffic_unit": "HBM bytes per step (conv family, PMC)", "traffic_source": os.path.relpath(p, ROOT)}
 
 
+def cpu_share() -> int:
+    """CPUs this process may actually use: its affinity mask, capped by a
+    cgroup CPU quota (the GPU box gives each one-GPU job a 16-CPU share while
+    os.cpu_count() and the affinity mask show the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")   # the box exports its share here too
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(args, res):
     from jr.inception import build_inception_v3
     from jr.init import init_params, unflatten
     from jr import synth
     from oracle.inception_ref import InceptionV3Ref
-    cores = min(16, os.cpu_count() or 1)
+    # every core this process may run on (the job's CPU share; os.cpu_count()
+    # is the whole machine's count, stated beside it)
+    cores = cpu_share()
     torch.set_num_threads(cores)
     g = build_inception_v3(res, res)
     ref = InceptionV3Ref(unflatten(g, init_params(g, 0)), torch.float32)
@@ -133,12 +210,16 @@ def cpu_baseline(args, res):
     st = {}
     ref.train_step(x, y, st)   # warm-up
     t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
+    for k in range(args.cpu_steps):
         ref.train_step(x, y, st)
+        log(f"cpu baseline step {k + 1}/{args.cpu_steps} on {cores} threads")
     dt = time.perf_counter() - t0
     return {"value": round(B * args.cpu_steps / dt, 3), "unit": "images/sec", "cores": cores, "kind": "port",
+            "host_cpu_count": os.cpu_count(),
             "sample": f"{args.cpu_steps} timed train steps (+1 warm-up) of batch {B} at {res}x{res} fp32, "
-                      f"torch-CPU restatement oracle/inception_ref.py ({dt:.1f} s)"}
+                      f"torch-CPU restatement oracle/inception_ref.py on {cores} threads = every CPU of this "
+                      f"job's share (affinity mask capped by the cgroup quota; os.cpu_count() = {os.cpu_count()}) "
+                      f"({dt:.1f} s)"}
 
 
 def main():
@@ -178,6 +259,7 @@ def main():
     labels = synth.labels(rank * B, B)
     eng.set_batch(imgs, labels)
     eng.synchronize()
+    log(f"engine ready (rank {rank}/{world})")
     ar = BucketAllReduce(eng, world) if world > 1 and train else None
     use_graph = (not args.no_graph) and ar is None
 
@@ -222,6 +304,7 @@ def main():
     if rank == 0:
         imgs_s = B * world * args.steps / elapsed
         ms = elapsed / args.steps * 1e3
+        log(f"timed {args.steps} steps: {ms:.3f} ms/step")
         roof = None
         if not args.no_roofline:
             flops, tconv, nconv = conv_roofline(eng)
@@ -234,6 +317,7 @@ def main():
                     "algorithmic_gflop_per_step": round(flops / 1e9, 1)}
             if train:
                 roof.update(pmc_traffic(args.dtype, B, res, math))
+        hbm = None if args.no_roofline else family_rates(eng)
         out = {
             "metric": (f"train images/sec, Inception-v3 {res}^2 bs{B}/GPU" if train else
                        f"eval images/sec, Inception-v3 {res}^2 bs{B}/GPU (one ensemble member, batch-stat BN)"),
@@ -249,8 +333,10 @@ def main():
                        "conv_math": CONV_MATH[args.conv_math] if args.dtype == "f32" else "bf16 MFMA"},
             ("final_loss" if train else "mean_prediction"): round(loss, 5),
             "roofline": roof,
+            "hbm_families": hbm,
         }
         if not args.no_cpu_baseline and world == 1 and train:
+            log("cpu baseline")
             out["cpu_baseline"] = cpu_baseline(args, res)
         print(json.dumps(out), flush=True)
     if dist:

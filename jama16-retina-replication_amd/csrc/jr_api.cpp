@@ -1,4 +1,5 @@
-// jr_api.cpp — library-level C-ABI: error convention, init, HIP graph capture.
+// jr_api.cpp — library-level C-ABI: init, launch-error mapping, HIP graph
+// capture (the error convention itself is host-only code: jr_error.cpp).
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -6,15 +7,6 @@
 #include "jr_common.h"
 
 namespace jr {
-
-static thread_local std::string g_last_error;
-
-void set_error(const std::string& msg) { g_last_error = msg; }
-
-int fail(int status, const std::string& msg) {
-  g_last_error = msg;
-  return status;
-}
 
 int check_launch(const char* what) {
   const hipError_t e = hipGetLastError();
@@ -25,8 +17,6 @@ int check_launch(const char* what) {
 }  // namespace jr
 
 using namespace jr;
-
-JR_API const char* jr_last_error(void) { return g_last_error.c_str(); }
 
 JR_API const char* jr_version(void) { return "libjr 0.2 gfx950 (implicit-GEMM conv: fp32 x8-split / fp32 / bf16 MFMA)"; }
 

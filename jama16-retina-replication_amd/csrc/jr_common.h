@@ -5,15 +5,10 @@
 #include <stdint.h>
 #include <string>
 
-#include "../../include/jr.h"
-
-#define JR_API extern "C" __attribute__((visibility("default")))
+#include "jr_error.h"
 
 namespace jr {
 
-// Thread-local last-error text (jr_last_error).
-void set_error(const std::string& msg);
-int fail(int status, const std::string& msg);
 // Map the last HIP launch error (if any) to JR_ERR_HIP.
 int check_launch(const char* what);
 

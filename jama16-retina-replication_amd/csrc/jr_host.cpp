@@ -9,7 +9,7 @@
 #include <stdint.h>
 #include <string.h>
 
-#include "jr_common.h"
+#include "jr_error.h"
 
 __attribute__((target("sse4.2"))) static uint32_t crc32c_sse(const uint8_t* p, size_t n, uint32_t crc) {
   crc = ~crc;

@@ -154,6 +154,33 @@ def load() -> ctypes.CDLL:
     return lib
 
 
+# host-only entry points (TFRecord / Example parsing, CRC32C, the error text):
+# no GPU involved; JR_HOST_LIB may point them at another build of the same
+# sources, e.g. the AddressSanitizer build (`make asan`, tests/test_asan_host.py)
+HOST_FUNCS = ("jr_last_error", "jr_crc32c", "jr_masked_crc32c", "jr_tfrecord_index", "jr_example_parse_image")
+_host = None
+
+
+def load_host() -> ctypes.CDLL:
+    global _host
+    if _host is not None:
+        return _host
+    path = os.environ.get("JR_HOST_LIB")
+    if not path:
+        _host = load()
+        return _host
+    lib = ctypes.CDLL(path)
+    for name in HOST_FUNCS:
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = _SIGS[name]
+    _host = lib
+    return lib
+
+
+def host_last_error() -> str:
+    return load_host().jr_last_error().decode(errors="replace")
+
+
 def last_error() -> str:
     return load().jr_last_error().decode(errors="replace")
 

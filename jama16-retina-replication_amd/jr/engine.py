@@ -382,8 +382,8 @@ class Engine:
         keep = []  # keep ctypes structs alive
         fwd, bwd, opt, seq = [], [], [], []
 
-        def add(lst, fn, args, name, lane, reads=(), writes=()):
-            c = Call(fn, args, name, lane, tuple(reads), tuple(writes))
+        def add(lst, fn, args, name, lane, reads=(), writes=(), nbytes=0):
+            c = Call(fn, args, name, lane, tuple(reads), tuple(writes), nbytes=int(nbytes))
             lst.append(c)
             seq.append(c)
 
@@ -424,7 +424,7 @@ class Engine:
                     src_stride = self.in_stride if u.x == g.input_buf else b.c
                     add(fwd, L.jr_split_x8p, (A(u.x), rows, b.c, 0, src_stride, AX(u.x), cp, 0, cp,
                                               self.batch * b.h * b.w * cp, s),
-                        "split_x8p", ln, a_all(u.x), [("ap", u.x)])
+                        "split_x8p", ln, a_all(u.x), [("ap", u.x)], nbytes=rows * (4 * b.c + 6 * cp))
                 # conv + the BN batch statistics of its raw output, fused
                 add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), cdt, AX(u.x), self._wf(u), raw, BN_EPS,
                                                     self.mean_unit[uid].data_ptr(),
@@ -436,17 +436,20 @@ class Engine:
                                                   self.invstd[m.idx].data_ptr(),
                                                   self._p(f"batch_normalization_{m.idx + 1}/beta"),
                                                   A(m.y.buf), m.y.c_off, yb.c, s),
-                        "bn_relu", ln, [("r", uid), ("p",)], [("a", m.y.buf, m.y.c_off)])
+                        "bn_relu", ln, [("r", uid), ("p",)], [("a", m.y.buf, m.y.c_off)],
+                        nbytes=2 * M * m.cout * self.esz)
             elif n.kind == "maxpool":
                 d = self._pool_desc(n, B)
                 keep.append(d)
                 add(fwd, L.jr_maxpool3x3s2_fwd, (ctypes.byref(d), dt, A(n.x), A(n.y.buf), self.argmax[i].data_ptr(), s),
-                    "maxpool_fwd", ln, a_all(n.x), [("a", n.y.buf, n.y.c_off), ("am", i)])
+                    "maxpool_fwd", ln, a_all(n.x), [("a", n.y.buf, n.y.c_off), ("am", i)],
+                    nbytes=B * n.c * (n.h * n.w * self.esz + n.ho * n.wo * (self.esz + 1)))
             else:
                 d = self._pool_desc(n, B)
                 keep.append(d)
                 add(fwd, L.jr_avgpool3x3s1_fwd, (ctypes.byref(d), dt, A(n.x), A(n.y.buf), s),
-                    "avgpool_fwd", ln, a_all(n.x), [("a", n.y.buf, n.y.c_off)])
+                    "avgpool_fwd", ln, a_all(n.x), [("a", n.y.buf, n.y.c_off)],
+                    nbytes=B * n.c * (n.h * n.w + n.ho * n.wo) * self.esz)
         ob = g.bufs[g.output_buf]
         s0 = S[0]
         add(fwd, L.jr_gap_fwd, (dt, A(g.output_buf), B, ob.h * ob.w, ob.c, self.feat.data_ptr(), s0),
@@ -486,12 +489,12 @@ class Engine:
                                                     self._p(f"batch_normalization_{m.idx + 1}/beta"), draw,
                                                     self._gp(f"batch_normalization_{m.idx + 1}/beta"), ws, wsb, s),
                             "bn_relu_bwd", ln, [("d", m.y.buf, m.y.c_off), ("r", uid), ("p",)],
-                            [("draw", ln), ("g", uid), ("ws", ln)])
+                            [("draw", ln), ("g", uid), ("ws", ln)], nbytes=3 * M * m.cout * self.esz)
                     dkey = ("draw", ln)
                     if x8p:             # the raw-output gradient as split planes (dgrad and wgrad operand)
                         drawp = self.drawp_lane[ln].data_ptr()
                         add(bwd, L.jr_split_x8p, (draw, M, u.cout, 0, u.cout, drawp, u.cout, 0, u.cout, M * u.cout, s),
-                            "split_x8p", ln, [("draw", ln)], [("drawp", ln)])
+                            "split_x8p", ln, [("draw", ln)], [("drawp", ln)], nbytes=10 * M * u.cout)
                         draw, dkey = drawp, ("drawp", ln)
                     add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), cdt, AX(u.x), draw,
                                                       self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
@@ -507,19 +510,22 @@ class Engine:
                     keep.append(d)
                     add(bwd, L.jr_maxpool3x3s2_bwd, (ctypes.byref(d), dt, self.argmax[i].data_ptr(), D(n.y.buf),
                                                      D(n.x), acc, s),
-                        "maxpool_bwd", ln, [("am", i), ("d", n.y.buf, n.y.c_off)], d_all(n.x))
+                        "maxpool_bwd", ln, [("am", i), ("d", n.y.buf, n.y.c_off)], d_all(n.x),
+                        nbytes=B * n.c * (n.ho * n.wo * (self.esz + 1) + n.h * n.w * self.esz * (1 + acc)))
                     written.add(n.x)
                 else:
                     d = self._pool_desc(n, B)
                     keep.append(d)
                     add(bwd, L.jr_avgpool3x3s1_bwd, (ctypes.byref(d), dt, D(n.y.buf), D(n.x), acc, s),
-                        "avgpool_bwd", ln, [("d", n.y.buf, n.y.c_off)], d_all(n.x))
+                        "avgpool_bwd", ln, [("d", n.y.buf, n.y.c_off)], d_all(n.x),
+                        nbytes=B * n.c * (n.ho * n.wo + n.h * n.w * (1 + acc)) * self.esz)
                     written.add(n.x)
             P, G = self.params.data_ptr(), self.grads.data_ptr()
             greads = [("g", u.first.idx) for u in self.cunits] + [("g", "dense")]
             if self.optimizer == "nesterov":
                 add(opt, L.jr_nesterov_update, (P, G, self.accum.data_ptr(), self.nparam, self.lr,
-                                                self.momentum, 1.0, s0), "nesterov", 0, greads, [("p",), ("acc",)])
+                                                self.momentum, 1.0, s0), "nesterov", 0, greads, [("p",), ("acc",)],
+                    nbytes=20 * self.nparam)
             elif self.optimizer == "momentum":
                 add(opt, L.jr_momentum_update, (P, G, self.accum.data_ptr(), self.nparam, self.lr,
                                                 self.momentum, 1.0, s0), "momentum", 0, greads, [("p",), ("acc",)])

@@ -41,6 +41,7 @@ class Call:
     writes: Tuple = ()
     idx: int = -1                                   # position in the step's call sequence
     waits: List[int] = field(default_factory=list)  # lanes whose work so far must finish first
+    nbytes: int = 0                                 # algorithmic HBM bytes (memory-bound ops; bench.py)
 
 
 def node_lanes(g, plan, nl: int) -> Dict[int, int]:

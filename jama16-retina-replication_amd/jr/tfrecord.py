@@ -29,6 +29,11 @@ from . import _ffi
 FeatureValue = Union[bytes, int, float, List[bytes], List[int], List[float], np.ndarray]
 
 
+def _check_host(name: str, rc: int) -> None:
+    if rc != _ffi.JR_OK:
+        raise _ffi.JRError(name, rc, _ffi.host_last_error())
+
+
 # ------------------------------------------------------------------ CRC32C
 def _ptr(data) -> bytes:
     # a bytes object is passed to the C-ABI as a pointer to its own buffer
@@ -37,13 +42,13 @@ def _ptr(data) -> bytes:
 
 
 def masked_crc32c(data: bytes) -> int:
-    lib = _ffi.load()
+    lib = _ffi.load_host()
     b = _ptr(data)
     return int(lib.jr_masked_crc32c(b, len(b)))
 
 
 def crc32c(data: bytes, crc: int = 0) -> int:
-    lib = _ffi.load()
+    lib = _ffi.load_host()
     b = _ptr(data)
     return int(lib.jr_crc32c(b, len(b), crc))
 
@@ -86,7 +91,7 @@ class RecordFile:
     raised on reaching it."""
 
     def __init__(self, path: str, verify: bool = True, parse: bool = True):
-        lib = _ffi.load()
+        lib = _ffi.load_host()
         self.path = path
         size = os.path.getsize(path)
         self._mm = None
@@ -99,7 +104,7 @@ class RecordFile:
         base = self.buf.ctypes.data
         n = ctypes.c_size_t(0)
         rc = lib.jr_tfrecord_index(base, size, int(verify), None, None, 0, ctypes.byref(n))
-        self.error = None if rc == 0 else _ffi.last_error()
+        self.error = None if rc == 0 else _ffi.host_last_error()
         cnt = n.value
         self.offsets = np.zeros(cnt, np.uint64)
         self.lengths = np.zeros(cnt, np.uint64)
@@ -116,7 +121,7 @@ class RecordFile:
             self.height = np.zeros(cnt, np.int64)
             self.width = np.zeros(cnt, np.int64)
             self.status = np.zeros(cnt, np.int32)
-            _ffi.check("jr_example_parse_image", lib.jr_example_parse_image(
+            _check_host("jr_example_parse_image", lib.jr_example_parse_image(
                 base, self.offsets.ctypes.data, self.lengths.ctypes.data, cnt, self.enc_off.ctypes.data,
                 self.enc_len.ctypes.data, self.label.ctypes.data, self.height.ctypes.data,
                 self.width.ctypes.data, self.status.ctypes.data))
