@@ -1,0 +1,276 @@
+// jr_jpeg.cpp — native JPEG decode for the input pipeline (libjr_jpeg.so,
+// host only; include/jr_jpeg.h).
+//
+// Replaces the decode half of tf.image.decode_jpeg at lib/dataset.py:20
+// (channels=0: the file's own channel count).  TF decodes with libjpeg-turbo,
+// dct_method "" = JDCT_IFAST, fancy upsampling on [TF-3P]; here the DCT
+// method is selectable (JR_JPEG_IFAST, the TF default, or JR_JPEG_ISLOW, what
+// Pillow uses).  The library linked is IJG libjpeg 9 (the only libjpeg with
+// headers in this image, /opt/conda).  Its IDCTs are the same integer
+// algorithms, but for subsampled chroma it scales the chroma IDCT up instead
+// of upsampling (and its colour conversion differs in detail), up to 65 LSB
+// away from libjpeg-turbo on 4:2:0 files.  So libjpeg 9 only runs the entropy
+// decode and the IDCT (raw_data_out: every component at its own resolution)
+// and this file does what libjpeg-turbo's decompressor does after that:
+// "fancy" triangle-filter upsampling of h2v1 / h2v2 chroma (jdsample.c:
+// 3/4 nearer + 1/4 further sample per dimension, the same rounding biases),
+// with edge rows / columns replicated as jdmainct.c provides them, and the
+// fixed-point YCbCr -> RGB tables of jdcolor.c (16 fraction bits).  Other
+// sampling layouts fall back to libjpeg 9's own output path.
+//
+// One call decodes one image straight into the caller's HWC uint8 buffer,
+// with no interpreter involvement: the pipeline's worker threads (ctypes
+// releases the GIL) decode in parallel.
+#include <algorithm>
+#include <csetjmp>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+extern "C" {
+#include <jpeglib.h>
+}
+
+#include "../../include/jr_jpeg.h"
+
+#define JR_JPEG_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+thread_local std::string g_err;
+
+struct ErrMgr {
+  jpeg_error_mgr pub;
+  jmp_buf jump;
+};
+
+void on_error(j_common_ptr cinfo) {
+  ErrMgr* e = reinterpret_cast<ErrMgr*>(cinfo->err);
+  char buf[JMSG_LENGTH_MAX];
+  (*cinfo->err->format_message)(cinfo, buf);
+  g_err = buf;
+  std::longjmp(e->jump, 1);
+}
+
+void on_message(j_common_ptr) {}   // corrupt-data warnings: libjpeg recovers; TF does the same
+
+// jdcolor.c build_ycc_rgb_table (SCALEBITS 16): R = y + Cr_r[cr],
+// G = y + ((Cb_g[cb] + Cr_g[cr]) >> 16), B = y + Cb_b[cb], clamped.
+struct YccTables {
+  int cr_r[256], cb_b[256];
+  long cr_g[256], cb_g[256];
+  YccTables() {
+    constexpr int SB = 16;
+    constexpr long HALF = 1L << (SB - 1);
+    auto fix = [](double x) { return (long)(x * (1L << SB) + 0.5); };
+    for (int i = 0, x = -128; i < 256; ++i, ++x) {
+      cr_r[i] = (int)((fix(1.40200) * x + HALF) >> SB);
+      cb_b[i] = (int)((fix(1.77200) * x + HALF) >> SB);
+      cr_g[i] = -fix(0.71414) * x;
+      cb_g[i] = -fix(0.34414) * x + HALF;
+    }
+  }
+};
+const YccTables& ycc() {
+  static const YccTables t;
+  return t;
+}
+inline uint8_t clamp255(long v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+// jdsample.c h2v1_fancy_upsample: one row, out has 2 * w samples
+void up_h2(const uint8_t* in, int w, uint8_t* out) {
+  if (w == 1) { out[0] = out[1] = in[0]; return; }
+  int v = in[0];
+  out[0] = (uint8_t)v;
+  out[1] = (uint8_t)((v * 3 + in[1] + 2) >> 2);
+  for (int c = 1; c < w - 1; ++c) {
+    v = in[c] * 3;
+    out[2 * c] = (uint8_t)((v + in[c - 1] + 1) >> 2);
+    out[2 * c + 1] = (uint8_t)((v + in[c + 1] + 2) >> 2);
+  }
+  v = in[w - 1];
+  out[2 * w - 2] = (uint8_t)((v * 3 + in[w - 2] + 1) >> 2);
+  out[2 * w - 1] = (uint8_t)v;
+}
+
+// jdsample.c h2v2_fancy_upsample: one output row from the nearest input row
+// (near) and the next nearest (far: the row above for the upper output row
+// of a pair, below for the lower one)
+void up_h2v2_row(const uint8_t* near, const uint8_t* far, int w, uint8_t* out) {
+  if (w == 1) {
+    const int s = near[0] * 3 + far[0];
+    out[0] = (uint8_t)((s * 4 + 8) >> 4);
+    out[1] = (uint8_t)((s * 4 + 7) >> 4);
+    return;
+  }
+  int this_s = near[0] * 3 + far[0], next_s = near[1] * 3 + far[1], last_s;
+  out[0] = (uint8_t)((this_s * 4 + 8) >> 4);
+  out[1] = (uint8_t)((this_s * 3 + next_s + 7) >> 4);
+  last_s = this_s;
+  this_s = next_s;
+  for (int c = 2; c < w; ++c) {
+    next_s = near[c] * 3 + far[c];
+    out[2 * c - 2] = (uint8_t)((this_s * 3 + last_s + 8) >> 4);
+    out[2 * c - 1] = (uint8_t)((this_s * 3 + next_s + 7) >> 4);
+    last_s = this_s;
+    this_s = next_s;
+  }
+  out[2 * w - 2] = (uint8_t)((this_s * 3 + last_s + 8) >> 4);
+  out[2 * w - 1] = (uint8_t)((this_s * 4 + 7) >> 4);
+}
+
+}  // namespace
+
+JR_JPEG_API const char* jr_jpeg_last_error(void) { return g_err.c_str(); }
+
+JR_JPEG_API int jr_jpeg_header(const uint8_t* data, size_t len, int32_t* height, int32_t* width, int32_t* channels) {
+  if (!data || !height || !width || !channels) {
+    g_err = "jr_jpeg_header: null argument";
+    return -1;
+  }
+  jpeg_decompress_struct cinfo;
+  ErrMgr err;
+  cinfo.err = jpeg_std_error(&err.pub);
+  err.pub.error_exit = on_error;
+  err.pub.output_message = on_message;
+  if (setjmp(err.jump)) {
+    jpeg_destroy_decompress(&cinfo);
+    return -1;
+  }
+  jpeg_create_decompress(&cinfo);
+  jpeg_mem_src(&cinfo, const_cast<uint8_t*>(data), (unsigned long)len);
+  jpeg_read_header(&cinfo, TRUE);
+  *height = (int32_t)cinfo.image_height;
+  *width = (int32_t)cinfo.image_width;
+  *channels = cinfo.num_components == 1 ? 1 : 3;
+  jpeg_destroy_decompress(&cinfo);
+  return 0;
+}
+
+JR_JPEG_API int jr_jpeg_decode(const uint8_t* data, size_t len, uint8_t* out, int32_t height, int32_t width,
+                               int32_t channels, int32_t dct_method) {
+  if (!data || !out || height <= 0 || width <= 0 || (channels != 1 && channels != 3)) {
+    g_err = "jr_jpeg_decode: bad arguments";
+    return -1;
+  }
+  if (dct_method != JR_JPEG_IFAST && dct_method != JR_JPEG_ISLOW) {
+    g_err = "jr_jpeg_decode: dct_method must be JR_JPEG_IFAST or JR_JPEG_ISLOW";
+    return -1;
+  }
+  jpeg_decompress_struct cinfo;
+  ErrMgr err;
+  cinfo.err = jpeg_std_error(&err.pub);
+  err.pub.error_exit = on_error;
+  err.pub.output_message = on_message;
+  if (setjmp(err.jump)) {
+    jpeg_destroy_decompress(&cinfo);
+    return -1;
+  }
+  jpeg_create_decompress(&cinfo);
+  jpeg_mem_src(&cinfo, const_cast<uint8_t*>(data), (unsigned long)len);
+  jpeg_read_header(&cinfo, TRUE);
+  cinfo.dct_method = dct_method == JR_JPEG_IFAST ? JDCT_IFAST : JDCT_ISLOW;
+  if ((int)cinfo.image_height != height || (int)cinfo.image_width != width ||
+      (cinfo.num_components == 1 ? 1 : 3) != channels) {
+    g_err = "jr_jpeg_decode: image is " + std::to_string(cinfo.image_height) + "x" +
+            std::to_string(cinfo.image_width) + "x" + std::to_string(cinfo.num_components == 1 ? 1 : 3) +
+            ", buffer " + std::to_string(height) + "x" + std::to_string(width) + "x" + std::to_string(channels);
+    jpeg_destroy_decompress(&cinfo);
+    return -1;
+  }
+  // the turbo-equivalent output path: YCbCr (or grayscale) files whose chroma
+  // is full, h2v1 or h2v2 subsampled
+  bool own = cinfo.jpeg_color_space == JCS_YCbCr && cinfo.num_components == 3;
+  if (own) {
+    const jpeg_component_info* cp = cinfo.comp_info;
+    const int H = cinfo.max_h_samp_factor, V = cinfo.max_v_samp_factor;
+    own = cp[0].h_samp_factor == H && cp[0].v_samp_factor == V && (H == 1 || H == 2) && (V == 1 || V == 2);
+    for (int k = 1; k < 3 && own; ++k) own = cp[k].h_samp_factor == 1 && cp[k].v_samp_factor == 1;
+  }
+  if (own) {
+    cinfo.raw_data_out = TRUE;
+    jpeg_start_decompress(&cinfo);
+    const int H = cinfo.max_h_samp_factor, V = cinfo.max_v_samp_factor;
+    const int lw = (int)cinfo.comp_info[0].width_in_blocks * DCTSIZE;
+    const int cw = (int)cinfo.comp_info[1].width_in_blocks * DCTSIZE;
+    const int lh = (int)cinfo.comp_info[0].height_in_blocks * DCTSIZE;
+    const int ch = (int)cinfo.comp_info[1].height_in_blocks * DCTSIZE;
+    const int rows_per_call = V * DCTSIZE;
+    // whole planes at component resolution (+ one iMCU row of slack)
+    std::vector<uint8_t> plane[3];
+    plane[0].resize((size_t)(lh + rows_per_call) * lw);
+    plane[1].resize((size_t)(ch + DCTSIZE) * cw);
+    plane[2].resize((size_t)(ch + DCTSIZE) * cw);
+    std::vector<JSAMPROW> ptrs[3];
+    ptrs[0].resize(rows_per_call);
+    ptrs[1].resize(DCTSIZE);
+    ptrs[2].resize(DCTSIZE);
+    int y0 = 0, c0 = 0;
+    while (cinfo.output_scanline < cinfo.output_height) {
+      for (int r = 0; r < rows_per_call; ++r) ptrs[0][r] = plane[0].data() + (size_t)(y0 + r) * lw;
+      for (int k = 1; k < 3; ++k)
+        for (int r = 0; r < DCTSIZE; ++r) ptrs[k][r] = plane[k].data() + (size_t)(c0 + r) * cw;
+      JSAMPARRAY arr[3] = {ptrs[0].data(), ptrs[1].data(), ptrs[2].data()};
+      if (jpeg_read_raw_data(&cinfo, arr, rows_per_call) == 0) break;
+      y0 += rows_per_call;
+      c0 += DCTSIZE;
+    }
+    // downsampled (valid) chroma geometry, as jdmaster.c computes it
+    const int dw = (width * 1 + H - 1) / H, dh = (height * 1 + V - 1) / V;
+    const YccTables& t = ycc();
+    std::vector<uint8_t> up_cb((size_t)2 * dw + 2), up_cr((size_t)2 * dw + 2);
+    for (int y = 0; y < height; ++y) {
+      const uint8_t* Y = plane[0].data() + (size_t)y * lw;
+      const uint8_t *cb, *cr;
+      if (H == 1 && V == 1) {
+        cb = plane[1].data() + (size_t)y * cw;
+        cr = plane[2].data() + (size_t)y * cw;
+      } else if (V == 1) {   // h2v1
+        up_h2(plane[1].data() + (size_t)y * cw, dw, up_cb.data());
+        up_h2(plane[2].data() + (size_t)y * cw, dw, up_cr.data());
+        cb = up_cb.data();
+        cr = up_cr.data();
+      } else {               // h2v2 (H == 2): row pair of chroma row cy
+        const int cy = y >> 1;
+        const int far = (y & 1) ? std::min(cy + 1, dh - 1) : std::max(cy - 1, 0);   // replicated edge rows
+        for (int k = 1; k < 3; ++k) {
+          const uint8_t* n = plane[k].data() + (size_t)cy * cw;
+          const uint8_t* f = plane[k].data() + (size_t)far * cw;
+          if (H == 2) up_h2v2_row(n, f, dw, (k == 1 ? up_cb : up_cr).data());
+        }
+        cb = up_cb.data();
+        cr = up_cr.data();
+      }
+      uint8_t* o = out + (size_t)y * width * 3;
+      for (int x = 0; x < width; ++x) {
+        const int yy = Y[x], b = cb[x], r = cr[x];
+        o[3 * x + 0] = clamp255(yy + t.cr_r[r]);
+        o[3 * x + 1] = clamp255(yy + (int)((t.cb_g[b] + t.cr_g[r]) >> 16));
+        o[3 * x + 2] = clamp255(yy + t.cb_b[b]);
+      }
+    }
+    jpeg_finish_decompress(&cinfo);
+    jpeg_destroy_decompress(&cinfo);
+    return 0;
+  }
+  cinfo.out_color_space = channels == 1 ? JCS_GRAYSCALE : JCS_RGB;
+  cinfo.do_fancy_upsampling = TRUE;
+  jpeg_start_decompress(&cinfo);
+  if ((int)cinfo.output_height != height || (int)cinfo.output_width != width ||
+      (int)cinfo.output_components != channels) {
+    g_err = "jr_jpeg_decode: image is " + std::to_string(cinfo.output_height) + "x" +
+            std::to_string(cinfo.output_width) + "x" + std::to_string(cinfo.output_components) + ", buffer " +
+            std::to_string(height) + "x" + std::to_string(width) + "x" + std::to_string(channels);
+    jpeg_destroy_decompress(&cinfo);
+    return -1;
+  }
+  const size_t row = (size_t)width * channels;
+  while (cinfo.output_scanline < cinfo.output_height) {
+    JSAMPROW r = out + (size_t)cinfo.output_scanline * row;
+    jpeg_read_scanlines(&cinfo, &r, 1);
+  }
+  jpeg_finish_decompress(&cinfo);
+  jpeg_destroy_decompress(&cinfo);
+  return 0;
+}

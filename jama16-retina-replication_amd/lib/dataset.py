@@ -28,9 +28,15 @@ handles and batches, and decodes only the batches b with b % world == rank
 -- the per-record JPEG work is split across ranks, the batch composition is
 that of the single-process stream.
 
-JPEG decoding [TF-3P]: TF's decode_jpeg defaults to libjpeg's IFAST DCT;
-Pillow uses ISLOW.  Pixels may differ by a few LSB from TF's decode — noted
-as unpinned in DESIGN.md.
+JPEG decoding [TF-3P]: TF's decode_jpeg defaults to libjpeg-turbo's IFAST
+IDCT.  The pipeline decodes natively (jr.jpeg, libjr_jpeg.so: IJG libjpeg 9
+entropy decode + IDCT, libjpeg-turbo's upsampling and colour conversion
+restated; outside the GIL, straight into the batch) with `jpeg_dct='ifast'`
+(TF's default; 'islow' selectable), and falls back to Pillow (libjpeg-turbo,
+ISLOW) when that library is not built (`jpeg_decoder='pillow'` forces it).
+With ISLOW the native bytes equal Pillow's (tests/test_data_pipeline.py);
+IFAST equals TF's decode to the extent IJG 9's AAN IDCT equals turbo's --
+no turbo IFAST decoder is importable here, so that last step is unpinned.
 """
 from __future__ import annotations
 
@@ -49,6 +55,7 @@ try:
 except ImportError:  # pragma: no cover
     Image = None
 
+from jr import jpeg as native_jpeg
 from jr import tfrecord
 
 _SCALE = np.float32(1.0 / 255.0)
@@ -68,13 +75,21 @@ def decode_jpeg(data: bytes) -> np.ndarray:
         return np.asarray(im, dtype=np.uint8)
 
 
-def _parse_example(record: bytes, image_dim, decode_dtype: str) -> Tuple[np.ndarray, np.ndarray]:
+def _decode_one(data, jpeg_decoder: Optional[str] = None, jpeg_dct: str = "ifast") -> np.ndarray:
+    """decode_jpeg by the pipeline's decoder (native when built, else Pillow)."""
+    if jpeg_decoder is None:
+        jpeg_decoder = "native" if native_jpeg.available() else "pillow"
+    return native_jpeg.decode(data, jpeg_dct) if jpeg_decoder == "native" else decode_jpeg(data)
+
+
+def _parse_example(record: bytes, image_dim, decode_dtype: str, jpeg_decoder: Optional[str] = None,
+                   jpeg_dct: str = "ifast") -> Tuple[np.ndarray, np.ndarray]:
     """lib/dataset.py:11-28."""
     ex = tfrecord.decode_example(record)
     for key in ("image/encoded", "image/format", "image/class/label", "image/height", "image/width"):
         if key not in ex or len(ex[key]) != 1:
             raise ValueError(f"record is missing FixedLenFeature {key!r}")
-    img = decode_jpeg(ex["image/encoded"][0])
+    img = _decode_one(ex["image/encoded"][0], jpeg_decoder, jpeg_dct)
     if img.size != int(np.prod(image_dim)):
         raise ValueError(f"cannot reshape image of {img.size} values into {list(image_dim)}")
     img = img.reshape(image_dim)                 # reshape, not transpose (App. C Q3)
@@ -90,13 +105,21 @@ class Dataset:
     def __init__(self, files: List[str], batch_size: int, num_epochs: int, num_workers: int,
                  prefetch_buffer_size: Optional[int], shuffle_buffer_size: Optional[int],
                  image_dim: List[int], seed: Optional[int], decode_dtype: str,
-                 shard: Optional[Tuple[int, int]] = None):
+                 shard: Optional[Tuple[int, int]] = None, jpeg_decoder: Optional[str] = None,
+                 jpeg_dct: str = "ifast"):
         if batch_size <= 0:
             raise ValueError("batch_size must be positive")
         rank, world = shard or (0, 1)
         if world < 1 or not 0 <= rank < world:
             raise ValueError(f"bad shard {shard!r}: need 0 <= rank < world")
         self.shard = (int(rank), int(world))
+        if jpeg_decoder is None:
+            jpeg_decoder = "native" if native_jpeg.available() else "pillow"
+        if jpeg_decoder not in ("native", "pillow") or jpeg_dct not in native_jpeg.DCT:
+            raise ValueError("jpeg_decoder: 'native' or 'pillow'; jpeg_dct: 'ifast' or 'islow'")
+        if jpeg_decoder == "native" and not native_jpeg.available():
+            raise RuntimeError("jpeg_decoder='native' needs libjr_jpeg.so (csrc Makefile)")
+        self.jpeg_decoder, self.jpeg_dct = jpeg_decoder, jpeg_dct
         self.files = files
         self.batch_size = int(batch_size)
         self.num_epochs = num_epochs
@@ -170,14 +193,26 @@ class Dataset:
             if b % world == rank:
                 yield items
 
+    def _decode(self, data: bytes, dst: Optional[np.ndarray]) -> np.ndarray:
+        """One JPEG: natively (straight into dst when it is a uint8 row of the
+        right size) or by Pillow."""
+        if self.jpeg_decoder == "native":
+            h, w, c = native_jpeg.header(data)
+            if dst is not None and dst.dtype == np.uint8 and dst.size == h * w * c:
+                return native_jpeg.decode(data, self.jpeg_dct, dst.reshape(-1)).reshape(h, w, c)
+            return native_jpeg.decode(data, self.jpeg_dct)
+        return decode_jpeg(data)
+
     def _decode_rows(self, items, rows, out) -> None:
         """map(_parse_example) for rows [rows) of one batch, written in place."""
         for r in rows:
             f, i = items[r]
             f.check(i)                                # FixedLenFeature checks (lib/dataset.py:12-16)
-            img = decode_jpeg(f.encoded(i))
+            img = self._decode(f.encoded(i), out[r] if self.decode_dtype == "uint8" else None)
             if img.size != out[r].size:
                 raise ValueError(f"cannot reshape image of {img.size} values into {self.image_dim}")
+            if img.base is not None and np.shares_memory(img, out[r]):
+                continue                              # decoded in place (uint8)
             img = img.reshape(self.image_dim)        # reshape, not transpose (App. C Q3)
             if self.decode_dtype == "float32":
                 np.multiply(img, _SCALE, out=out[r])  # convert_image_dtype: f32(x) * f32(1/255)
@@ -327,7 +362,7 @@ def initialize_dataset(image_dir, batch_size, num_epochs=1,
                        shuffle_buffer_size=None,
                        image_data_format='channels_last',
                        num_channels=3, image_dim=[299, 299], *,
-                       seed=None, decode_dtype="float32", shard=None):
+                       seed=None, decode_dtype="float32", shard=None, jpeg_decoder=None, jpeg_dct="ifast"):
     """lib/dataset.py:31-59 (same arguments, same order, same defaults)."""
     files = _tfrecord_files_from_folder(image_dir)
     if image_data_format == 'channels_first':
@@ -339,7 +374,7 @@ def initialize_dataset(image_dir, batch_size, num_epochs=1,
     if decode_dtype not in ("float32", "uint8"):
         raise ValueError("decode_dtype must be 'float32' or 'uint8'")
     return Dataset(files, batch_size, num_epochs, num_workers, prefetch_buffer_size,
-                   shuffle_buffer_size, dim, seed, decode_dtype, shard)
+                   shuffle_buffer_size, dim, seed, decode_dtype, shard, jpeg_decoder, jpeg_dct)
 
 
 def close_iterator(it) -> None:

@@ -245,8 +245,8 @@ def test_shards_partition_the_stream_and_decode_only_their_batches(records, monk
     repeated)."""
     import lib.dataset as D
     calls = []
-    real = D.decode_jpeg
-    monkeypatch.setattr(D, "decode_jpeg", lambda data: (calls.append(1), real(data))[1])
+    real = D.Dataset._decode
+    monkeypatch.setattr(D.Dataset, "_decode", lambda self, data, dst: (calls.append(1), real(self, data, dst))[1])
     kw = dict(image_dim=[64, 64], shuffle_buffer_size=16, seed=9, decode_dtype="uint8")
     full = D.initialize_dataset(records, 4, **kw)
     ref = [list(full) for _ in range(2)]                       # two epochs
@@ -296,3 +296,54 @@ def test_prefetch_close_stops_the_pipeline(records):
         with pytest.raises(StopIteration):
             next(it)
     assert threading.active_count() <= before + 1
+
+
+def test_native_jpeg_decoder(records):
+    """libjr_jpeg (IJG libjpeg 9 entropy decode + IDCT, then libjpeg-turbo's
+    fancy upsampling and fixed-point colour conversion restated in
+    jr_jpeg.cpp; outside the GIL).  With the same IDCT (ISLOW) the pixels are
+    BIT-IDENTICAL to Pillow's libjpeg-turbo decode for 4:4:4, 4:2:2 and 4:2:0
+    files, odd sizes included (edge columns / rows of the triangle filter).
+    (Linking libjpeg 9's own output path instead differs by up to 65 LSB on
+    4:2:0: it scales the chroma IDCT up rather than upsampling.)  TF's default
+    IFAST IDCT stays within a few LSB of ISLOW.  The pipeline decodes in place
+    either way and its labels / shapes are unchanged."""
+    import io
+    from PIL import Image
+    import lib.dataset as D
+    from jr import jpeg as J
+    if not J.available():
+        pytest.skip("libjr_jpeg.so not built")
+    rng = np.random.default_rng(0)
+    fast_dev = []
+    for h, w in ((61, 77), (64, 64), (17, 33), (1, 9)):
+        img = np.clip(rng.normal(120, 40, (h, w, 3)), 0, 255).astype(np.uint8)
+        for sub in (0, 1, 2):                                 # 4:4:4, 4:2:2, 4:2:0
+            buf = io.BytesIO()
+            Image.fromarray(img).save(buf, "JPEG", quality=95, subsampling=sub)
+            data = buf.getvalue()
+            pil = D.decode_jpeg(data).astype(int)
+            islow = J.decode(data, "islow").astype(int)
+            ifast = J.decode(data, "ifast").astype(int)
+            assert islow.shape == pil.shape == (h, w, 3)
+            assert np.array_equal(islow, pil), (h, w, sub, np.abs(islow - pil).max())
+            assert np.abs(ifast - islow).max() <= 8
+            fast_dev.append(np.abs(ifast - islow).ravel())
+    assert np.concatenate(fast_dev).mean() < 1.0
+    gray = io.BytesIO()
+    g = np.clip(rng.normal(120, 40, (61, 77)), 0, 255).astype(np.uint8)
+    Image.fromarray(g).save(gray, "JPEG", quality=90)
+    dg = J.decode(gray.getvalue(), "islow")
+    assert dg.shape == (61, 77, 1)
+    np.testing.assert_array_equal(dg[..., 0], np.asarray(Image.open(io.BytesIO(gray.getvalue()))))
+    with pytest.raises(ValueError):
+        J.decode(b"\xff\xd8 not a jpeg")
+    kw = dict(image_dim=[64, 64], decode_dtype="uint8")
+    a = list(D.initialize_dataset(records, 8, jpeg_decoder="native", **kw))
+    b = list(D.initialize_dataset(records, 8, jpeg_decoder="pillow", **kw))
+    for (xa, ya), (xb, yb) in zip(a, b):
+        np.testing.assert_array_equal(ya, yb)
+        assert xa.shape == xb.shape
+    c = list(D.initialize_dataset(records, 8, jpeg_decoder="native", jpeg_dct="islow", **kw))
+    for (xc, _), (xb, _) in zip(c, b):
+        np.testing.assert_array_equal(xc, xb)              # ISLOW: the pipeline's bytes == Pillow's
