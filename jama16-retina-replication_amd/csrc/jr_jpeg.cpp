@@ -55,28 +55,35 @@ void on_error(j_common_ptr cinfo) {
 
 void on_message(j_common_ptr) {}   // corrupt-data warnings: libjpeg recovers; TF does the same
 
-// jdcolor.c build_ycc_rgb_table (SCALEBITS 16): R = y + Cr_r[cr],
-// G = y + ((Cb_g[cb] + Cr_g[cr]) >> 16), B = y + Cb_b[cb], clamped.
-struct YccTables {
-  int cr_r[256], cb_b[256];
-  long cr_g[256], cb_g[256];
-  YccTables() {
-    constexpr int SB = 16;
-    constexpr long HALF = 1L << (SB - 1);
-    auto fix = [](double x) { return (long)(x * (1L << SB) + 0.5); };
-    for (int i = 0, x = -128; i < 256; ++i, ++x) {
-      cr_r[i] = (int)((fix(1.40200) * x + HALF) >> SB);
-      cb_b[i] = (int)((fix(1.77200) * x + HALF) >> SB);
-      cr_g[i] = -fix(0.71414) * x;
-      cb_g[i] = -fix(0.34414) * x + HALF;
-    }
+// jdcolor.c build_ycc_rgb_table (SCALEBITS 16): the tables hold
+//   Cr_r[cr] = (FIX(1.40200) * x + HALF) >> 16,  Cb_b[cb] = (FIX(1.77200) * x + HALF) >> 16,
+//   Cr_g[cr] = -FIX(0.71414) * x,                Cb_g[cb] = -FIX(0.34414) * x + HALF
+// (x = sample - 128), and R = y + Cr_r, G = y + ((Cb_g + Cr_g) >> 16),
+// B = y + Cb_b, clamped.  Computed inline (the same int32 values, arithmetic
+// shifts) so the row loop vectorises.
+constexpr int kFixCrR = 91881, kFixCbB = 116130, kFixCrG = 46802, kFixCbG = 22554, kHalf = 1 << 15;
+static_assert(kFixCrR == (int)(1.40200 * 65536 + 0.5) && kFixCbB == (int)(1.77200 * 65536 + 0.5) &&
+                  kFixCrG == (int)(0.71414 * 65536 + 0.5) && kFixCbG == (int)(0.34414 * 65536 + 0.5),
+              "jdcolor.c FIX() constants");
+
+inline int clamp255(int v) { return v < 0 ? 0 : v > 255 ? 255 : v; }
+
+// one output row; planar R/G/B first (three vectorisable loops), then interleaved
+void ycc_row(const uint8_t* __restrict Y, const uint8_t* __restrict cb, const uint8_t* __restrict cr, int w,
+             uint8_t* __restrict rgb, uint8_t* __restrict tmp) {
+  uint8_t* __restrict R = tmp;
+  uint8_t* __restrict G = tmp + w;
+  uint8_t* __restrict B = tmp + 2 * w;
+  for (int x = 0; x < w; ++x) R[x] = (uint8_t)clamp255(Y[x] + ((kFixCrR * (cr[x] - 128) + kHalf) >> 16));
+  for (int x = 0; x < w; ++x)
+    G[x] = (uint8_t)clamp255(Y[x] + ((-kFixCbG * (cb[x] - 128) + kHalf - kFixCrG * (cr[x] - 128)) >> 16));
+  for (int x = 0; x < w; ++x) B[x] = (uint8_t)clamp255(Y[x] + ((kFixCbB * (cb[x] - 128) + kHalf) >> 16));
+  for (int x = 0; x < w; ++x) {
+    rgb[3 * x] = R[x];
+    rgb[3 * x + 1] = G[x];
+    rgb[3 * x + 2] = B[x];
   }
-};
-const YccTables& ycc() {
-  static const YccTables t;
-  return t;
 }
-inline uint8_t clamp255(long v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
 
 // jdsample.c h2v1_fancy_upsample: one row, out has 2 * w samples
 void up_h2(const uint8_t* in, int w, uint8_t* out) {
@@ -96,28 +103,20 @@ void up_h2(const uint8_t* in, int w, uint8_t* out) {
 
 // jdsample.c h2v2_fancy_upsample: one output row from the nearest input row
 // (near) and the next nearest (far: the row above for the upper output row
-// of a pair, below for the lower one)
-void up_h2v2_row(const uint8_t* near, const uint8_t* far, int w, uint8_t* out) {
-  if (w == 1) {
-    const int s = near[0] * 3 + far[0];
-    out[0] = (uint8_t)((s * 4 + 8) >> 4);
-    out[1] = (uint8_t)((s * 4 + 7) >> 4);
-    return;
+// of a pair, below for the lower one).  Column sums s[c] = 3 near + far, then
+// out[2c] = (3 s[c] + s[c-1] + 8) >> 4, out[2c+1] = (3 s[c] + s[c+1] + 7) >> 4,
+// with s[-1] -> s[0] and s[w] -> s[w-1] at the edges (turbo writes those two
+// as (4 s + 8) >> 4 and (4 s + 7) >> 4: the same values).
+void up_h2v2_row(const uint8_t* __restrict near, const uint8_t* __restrict far, int w, uint8_t* __restrict out,
+                 int16_t* __restrict s) {
+  for (int c = 0; c < w; ++c) s[c + 1] = (int16_t)(near[c] * 3 + far[c]);
+  s[0] = s[1];
+  s[w + 1] = s[w];
+  for (int c = 0; c < w; ++c) {
+    const int t = s[c + 1] * 3;
+    out[2 * c] = (uint8_t)((t + s[c] + 8) >> 4);
+    out[2 * c + 1] = (uint8_t)((t + s[c + 2] + 7) >> 4);
   }
-  int this_s = near[0] * 3 + far[0], next_s = near[1] * 3 + far[1], last_s;
-  out[0] = (uint8_t)((this_s * 4 + 8) >> 4);
-  out[1] = (uint8_t)((this_s * 3 + next_s + 7) >> 4);
-  last_s = this_s;
-  this_s = next_s;
-  for (int c = 2; c < w; ++c) {
-    next_s = near[c] * 3 + far[c];
-    out[2 * c - 2] = (uint8_t)((this_s * 3 + last_s + 8) >> 4);
-    out[2 * c - 1] = (uint8_t)((this_s * 3 + next_s + 7) >> 4);
-    last_s = this_s;
-    this_s = next_s;
-  }
-  out[2 * w - 2] = (uint8_t)((this_s * 3 + last_s + 8) >> 4);
-  out[2 * w - 1] = (uint8_t)((this_s * 4 + 7) >> 4);
 }
 
 }  // namespace
@@ -218,8 +217,8 @@ JR_JPEG_API int jr_jpeg_decode(const uint8_t* data, size_t len, uint8_t* out, in
     }
     // downsampled (valid) chroma geometry, as jdmaster.c computes it
     const int dw = (width * 1 + H - 1) / H, dh = (height * 1 + V - 1) / V;
-    const YccTables& t = ycc();
-    std::vector<uint8_t> up_cb((size_t)2 * dw + 2), up_cr((size_t)2 * dw + 2);
+    std::vector<uint8_t> up_cb((size_t)2 * dw + 2), up_cr((size_t)2 * dw + 2), tmp((size_t)3 * width);
+    std::vector<int16_t> colsum((size_t)dw + 2);
     for (int y = 0; y < height; ++y) {
       const uint8_t* Y = plane[0].data() + (size_t)y * lw;
       const uint8_t *cb, *cr;
@@ -237,18 +236,12 @@ JR_JPEG_API int jr_jpeg_decode(const uint8_t* data, size_t len, uint8_t* out, in
         for (int k = 1; k < 3; ++k) {
           const uint8_t* n = plane[k].data() + (size_t)cy * cw;
           const uint8_t* f = plane[k].data() + (size_t)far * cw;
-          if (H == 2) up_h2v2_row(n, f, dw, (k == 1 ? up_cb : up_cr).data());
+          up_h2v2_row(n, f, dw, (k == 1 ? up_cb : up_cr).data(), colsum.data());
         }
         cb = up_cb.data();
         cr = up_cr.data();
       }
-      uint8_t* o = out + (size_t)y * width * 3;
-      for (int x = 0; x < width; ++x) {
-        const int yy = Y[x], b = cb[x], r = cr[x];
-        o[3 * x + 0] = clamp255(yy + t.cr_r[r]);
-        o[3 * x + 1] = clamp255(yy + (int)((t.cb_g[b] + t.cr_g[r]) >> 16));
-        o[3 * x + 2] = clamp255(yy + t.cb_b[b]);
-      }
+      ycc_row(Y, cb, cr, width, out + (size_t)y * width * 3, tmp.data());
     }
     jpeg_finish_decompress(&cinfo);
     jpeg_destroy_decompress(&cinfo);
