@@ -58,6 +58,9 @@ def parse():
                          "(jr.h JR_F32_X8, fp32-accurate); f32: fp32 MFMA")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a HIP graph")
     ap.add_argument("--lanes", type=int, default=2, help="streams for branch-level concurrency (jr.lanes)")
+    ap.add_argument("--tiles", default="pinned", choices=["pinned", "heuristic", "autotune"],
+                    help="conv tiles: the committed MI355X table of this workload (train.py's default; "
+                         "deterministic, bit-stable across boxes), the planner heuristic, or timed autotuning")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=64)
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -254,7 +257,7 @@ def main():
     B, res = args.batch or (64 if train else 32), args.res
     math = args.conv_math if args.dtype == "f32" else "bf16"
     eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0, lanes=args.lanes, train=train,
-                 conv_math=math)
+                 conv_math=math, tiles=args.tiles)
     imgs = synth.fundus_batch(rank * B, B, res)
     labels = synth.labels(rank * B, B)
     eng.set_batch(imgs, labels)
@@ -330,6 +333,7 @@ def main():
                                     f"Inception-v3 {res}x{res} {args.dtype} forward (evaluate.py), batch {B}/GPU, "
                                     f"batches sharded over ranks"), "model": "inception_v3", "global_batch": B * world,
                        "seq_len": None, "parallelism": f"dp{world}", "hip_graph": use_graph, "lanes": args.lanes,
+                       "tiles": eng.tiles,
                        "conv_math": CONV_MATH[args.conv_math] if args.dtype == "f32" else "bf16 MFMA"},
             ("final_loss" if train else "mean_prediction"): round(loss, 5),
             "roofline": roof,

@@ -80,15 +80,16 @@ def expand_model_paths(load_model_path: str):
 
 
 def make_engines(paths, meta, batch_size, device=0, conv_math="x8"):
-    """One inference engine per ensemble member, parameters loaded; the first
-    autotunes the conv tiles, the others reuse them (libjr's tile cache is
-    per geometry)."""
+    """One inference engine per ensemble member, parameters loaded; conv
+    tiles from the committed MI355X table of the eval workload (Engine
+    tiles="pinned"; the heuristic where none matches): every member and every
+    run sums in the same order."""
     from jr import checkpoint
     from jr.engine import Engine
     engines = []
-    for k, path in enumerate(paths):
+    for path in paths:
         eng = Engine(batch_size, meta["height"], meta["width"], meta.get("units", 1), device=device,
-                     train=False, conv_math=conv_math, autotune=(k == 0))
+                     train=False, conv_math=conv_math)
         flat, _ = checkpoint.load(path, eng.g)
         eng.load_params(flat)
         engines.append(eng)

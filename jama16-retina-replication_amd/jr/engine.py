@@ -25,6 +25,8 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
+import json
+import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
@@ -39,6 +41,22 @@ from .plan import ConvUnit, build_plan
 DTYPES = {"f32": _ffi.JR_F32, "bf16": _ffi.JR_BF16}
 
 
+_PINNED = None
+
+
+def pinned_tile_table(conv_math: str, batch: int, height: int, width: int, train: bool) -> Optional[dict]:
+    """The committed tile table (jr/tiles_mi355x.json) of this workload, or None."""
+    global _PINNED
+    if _PINNED is None:
+        p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tiles_mi355x.json")
+        _PINNED = json.load(open(p))["tables"] if os.path.exists(p) else []
+    for t in _PINNED:
+        if (t["conv_math"], t["batch"], t["height"], t["width"], t["train"]) == (conv_math, batch, height, width,
+                                                                              train):
+            return t
+    return None
+
+
 class Engine:
     """One model replica on one GPU (one process per GPU)."""
 
@@ -46,7 +64,7 @@ class Engine:
                  device: int | torch.device = 0, dtype: str = "f32", train: bool = True,
                  optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
                  head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None,
-                 autotune: bool = True, fuse_siblings: bool = True, lanes: int = 2,
+                 autotune: bool = False, tiles: str = "pinned", fuse_siblings: bool = True, lanes: int = 2,
                  conv_math: Optional[str] = None):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
@@ -96,8 +114,25 @@ class Engine:
         self._calls: Dict[int, Tuple[list, list, list]] = {}
         self._graphs: Dict[int, int] = {}
         self.bucket_hooks: List[Tuple[int, Callable]] = []
+        # conv tiles: "pinned" = the committed MI355X table for this workload
+        # (jr/tiles_mi355x.json, tools/make_tile_tables.py) when there is one,
+        # else the planner heuristic -- both deterministic, so every run on
+        # every box sums in the same order; "autotune" (or autotune=True)
+        # times the candidates on this box (fastest, box-dependent order)
+        if tiles not in ("pinned", "heuristic", "autotune"):
+            raise ValueError("tiles: 'pinned', 'heuristic' or 'autotune'")
         if autotune:
+            tiles = "autotune"
+        self.tiles = "heuristic"
+        self.clear_tile_table()         # libjr's per-geometry overrides are process-wide
+        if tiles == "autotune":
             self.autotune()
+            self.tiles = "autotune"
+        elif tiles == "pinned":
+            t = pinned_tile_table(self.conv_math, self.batch, self.g.height, self.g.width, self.train_mode)
+            if t is not None and all(u.name in t["configs"] for u in self.cunits):
+                self.set_tile_table(t)
+                self.tiles = "pinned"
 
     # ------------------------------------------------------------------ memory
     def _t(self, n: int, dtype=torch.float32) -> torch.Tensor:

@@ -71,10 +71,12 @@ def build_parser():
     p.add_argument("--conv_math", default="x8", choices=["x8", "x8p", "f32"],
                    help="fp32 convolution arithmetic: x8 = exact 3-way bf16 split on the matrix cores (fp32-accurate, "
                         "default), x8p = the same on pre-split operand planes, f32 = fp32 MFMA")
-    p.add_argument("--tiles", default="heuristic", choices=["heuristic", "autotune"],
-                   help="conv tile configs: heuristic (default; a function of the layer shapes only, so two runs on "
-                        "any MI355X sum in the same order and train bitwise-equal) or autotune (timed on rank 0 at "
-                        "start, broadcast to every rank); the table in use is saved in the checkpoint .meta")
+    p.add_argument("--tiles", default="pinned", choices=["pinned", "heuristic", "autotune"],
+                   help="conv tile configs: pinned (default; the committed MI355X table of this workload, "
+                        "jr/tiles_mi355x.json, else the heuristic), heuristic (a function of the layer shapes only) "
+                        "-- with either, two runs on any MI355X sum in the same order and train bitwise-equal -- or "
+                        "autotune (timed on rank 0 at start, broadcast to every rank); the table in use is saved in "
+                        "the checkpoint .meta")
     p.add_argument("--tile_table", default=None,
                    help="checkpoint path (or JSON file) whose saved tile table to reuse: reproduces that run's "
                         "summation order exactly")
@@ -162,8 +164,8 @@ Use SGD: {bool(args.vanilla_sgd)}
 
     engine = Engine(max(TRAIN_BATCH_SIZE, VAL_BATCH_SIZE), args.image_size, args.image_size,
                     device=local, optimizer="sgd" if args.vanilla_sgd else ("nesterov" if USE_NESTEROV else "momentum"),
-                    lr=LEARNING_RATE, momentum=MOMENTUM, seed=args.seed, conv_math=args.conv_math, autotune=False)
-    engine.clear_tile_table()
+                    lr=LEARNING_RATE, momentum=MOMENTUM, seed=args.seed, conv_math=args.conv_math,
+                    tiles="pinned" if args.tiles == "pinned" else "heuristic")
     table = None
     if args.tile_table:
         table = load_tile_table(args.tile_table)

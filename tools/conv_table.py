@@ -67,10 +67,10 @@ for (u, op, f), (r, t, t2) in zip(seq, last):
     tot_t += t + t2; tot_f += f
     name = r["Kernel_Name"]; cfg = name[name.index("<"):name.index(">") + 1]
     out.append((t + t2, f"{u.name:14s} {op:5s} {u.kh}x{u.kw}/{u.stride} {u.h:3d}x{u.w:<3d} {u.cin:4d}->{u.cout:4d} "
-                f"{cfg:24s} grid={r['Grid_Size_X']:>7s}x{r['Grid_Size_Z']:<4s} {t/1e3:8.1f}+{t2/1e3:6.1f}us {f/(t+t2)/1e3:7.1f} TF/s"))
+                f"{cfg:24s} grid={r['Grid_Size_X']:>7s}x{r['Grid_Size_Z']:<4s} {t/1e3:8.1f}+{t2/1e3:6.1f}us {f/max(t+t2, 1)/1e3:7.1f} TF/s"))
 for t, s in sorted(out, reverse=True)[:int(sys.argv[3]) if len(sys.argv) > 3 else 40]:
     print(s)
-print(f"total conv {tot_t/1e6:.2f} ms, {tot_f/tot_t/1e3:.1f} TF/s")
+print(f"total conv {tot_t/1e6:.2f} ms, {tot_f/max(tot_t, 1)/1e3:.1f} TF/s")
 
 # ---- whole-step breakdown: kernels between the last two optimizer launches
 opt = [i for i, r in enumerate(rows) if "k_nesterov" in r["Kernel_Name"] or "k_sgd" in r["Kernel_Name"]]
