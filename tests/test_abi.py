@@ -9,8 +9,8 @@ import pytest
 from conftest import ROOT
 
 
-def header_symbols():
-    text = open(os.path.join(ROOT, "include", "jr.h")).read()
+def header_symbols(name="jr.h"):
+    text = open(os.path.join(ROOT, "include", name)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(jr_[a-z0-9_]+)\s*\(", text)))
 
@@ -30,6 +30,17 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # and the ctypes binding covers the same surface
     assert set(_ffi.EXPORTED) >= set(header_symbols()) - {"jr_conv2d_debug_time"}
+
+
+def test_jpeg_library_exports_every_declared_symbol():
+    """include/jr_jpeg.h -> libjr_jpeg.so (host-only, built by the same Makefile)."""
+    from jr import jpeg
+    assert jpeg.available(), "libjr_jpeg.so not built"
+    lib = ctypes.CDLL(jpeg.LIB_PATH)
+    syms = header_symbols("jr_jpeg.h")
+    assert {"jr_jpeg_header", "jr_jpeg_decode", "jr_jpeg_last_error"} <= set(syms)
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
 
 
 def test_validation_errors_without_gpu():
