@@ -419,7 +419,7 @@ static void launch_tile(bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) 
 
 template <int OP, int NP>
 static void launch_op_bf16(int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  static_assert(kNumCfgsBf16 == 10 && kNumCfgsX8P == 10, "keep the switch in sync with kCfgsBf16 / kCfgsX8P");
+  static_assert(kNumCfgsBf16 == 14 && kNumCfgsX8P == 14, "keep the switch in sync with kCfgsBf16 / kCfgsX8P");
   switch (tile) {
     case 0: launch_tile<OP, 0, NP>(fast, a, grid, s); break;
     case 1: launch_tile<OP, 1, NP>(fast, a, grid, s); break;
@@ -430,7 +430,11 @@ static void launch_op_bf16(int tile, bool fast, const ConvArgs& a, dim3 grid, hi
     case 6: launch_tile<OP, 6, NP>(fast, a, grid, s); break;
     case 7: launch_tile<OP, 7, NP>(fast, a, grid, s); break;
     case 8: launch_tile<OP, 8, NP>(fast, a, grid, s); break;
-    default: launch_tile<OP, 9, NP>(fast, a, grid, s); break;
+    case 9: launch_tile<OP, 9, NP>(fast, a, grid, s); break;
+    case 10: launch_tile<OP, 10, NP>(fast, a, grid, s); break;
+    case 11: launch_tile<OP, 11, NP>(fast, a, grid, s); break;
+    case 12: launch_tile<OP, 12, NP>(fast, a, grid, s); break;
+    default: launch_tile<OP, 13, NP>(fast, a, grid, s); break;
   }
 }
 

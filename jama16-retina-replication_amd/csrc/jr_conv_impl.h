@@ -422,6 +422,14 @@ static constexpr TileCfg kCfgsBf16[] = {
     // 64 x 64 wave tiles issue 0.5: the per-MFMA issue budget is the bound)
     {256, 256, 2, 32, 3, 1.10},  // 8: wave 128x128, 96 KiB
     {256, 192, 2, 32, 3, 1.08},  // 9: wave 128x96, 84 KiB
+    // deeper rings for the short-K-loop 17x17 / 8x8 GEMMs, whose K-tiles
+    // carry few MFMAs per wave: NBUF - 2 stages stay in flight under the
+    // compute of one (eff just below the same-shape tile above: the untuned
+    // planner keeps its choice, autotuning / the pinned tables decide)
+    {128, 64, 2, 32, 5, 0.91},   // 10: 60 KiB, 3 stages in flight
+    {128, 128, 2, 32, 4, 0.99},  // 11: 64 KiB, 2 in flight
+    {128, 96, 4, 32, 5, 0.89},   // 12: 70 KiB
+    {128, 64, 2, 64, 3, 0.91},   // 13: 72 KiB, twice the MFMAs per K-tile
 };
 constexpr int kNumCfgsBf16 = sizeof(kCfgsBf16) / sizeof(kCfgsBf16[0]);
 
@@ -439,6 +447,10 @@ static constexpr TileCfg kCfgsX8P[] = {
     {64, 64, 2, 32, 3, 0.75},    // 7: wave 32x32, 72 KiB
     {256, 256, 2, 16, 2, 1.10},  // 8: wave 128x128, 96 KiB
     {256, 192, 2, 16, 3, 1.08},  // 9: wave 128x96, 126 KiB
+    {128, 64, 2, 16, 5, 0.91},   // 10: 90 KiB (deeper rings, as kCfgsBf16 10-13)
+    {128, 128, 2, 16, 5, 0.99},  // 11: 120 KiB
+    {128, 96, 4, 16, 4, 0.89},   // 12: 84 KiB
+    {128, 64, 2, 32, 3, 0.91},   // 13: 108 KiB
 };
 constexpr int kNumCfgsX8P = sizeof(kCfgsX8P) / sizeof(kCfgsX8P[0]);
 
