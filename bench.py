@@ -264,7 +264,7 @@ def main():
     eng.synchronize()
     log(f"engine ready (rank {rank}/{world})")
     ar = BucketAllReduce(eng, world) if world > 1 and train else None
-    use_graph = (not args.no_graph) and ar is None
+    use_graph = (not args.no_graph) and ar is None and args.lanes <= 2   # graphs: at most two lanes (jr.engine.capture)
 
     def step():
         if use_graph:

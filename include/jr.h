@@ -297,11 +297,6 @@ int jr_comm_destroy(jr_comm* comm);
 int jr_graph_begin(void* stream);
 int jr_graph_end(void* stream, void** graph_exec);
 int jr_graph_launch(void* graph_exec, void* stream);
-/* Explicit DAG capture on one stream (the lanes of a step as graph branches):
- * read the capturing stream's current dependency set (the nodes the next
- * captured operation will depend on), or replace it. */
-int jr_graph_get_deps(void* stream, void** nodes, int max_nodes, int* n_out);
-int jr_graph_set_deps(void* stream, void* const* nodes, int n);
 int jr_graph_destroy(void* graph_exec);
 
 #ifdef __cplusplus

@@ -54,34 +54,6 @@ JR_API int jr_graph_end(void* stream, void** graph_exec) {
   return JR_OK;
 }
 
-// Explicit DAG capture on ONE stream: the engine sets the stream's capture
-// dependency set before each call (its lane's tail plus the tails of the
-// lanes it waits for) and reads the call's new nodes back afterwards.  This
-// builds the lanes' graph without multi-stream capture (event waits across
-// three or more captured streams crashed hipGraphInstantiate on ROCm 7.2).
-JR_API int jr_graph_get_deps(void* stream, void** nodes, int max_nodes, int* n_out) {
-  if (!nodes || !n_out || max_nodes < 0) return fail(JR_ERR_INVALID, "graph_get_deps: bad arguments");
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  const hipGraphNode_t* deps = nullptr;
-  size_t n = 0;
-  const hipError_t e = hipStreamGetCaptureInfo_v2(as_stream(stream), &st, nullptr, nullptr, &deps, &n);
-  if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("graph_get_deps: ") + hipGetErrorString(e));
-  if (st != hipStreamCaptureStatusActive) return fail(JR_ERR_INVALID, "graph_get_deps: stream is not capturing");
-  if (n > (size_t)max_nodes) return fail(JR_ERR_INVALID, "graph_get_deps: more dependencies than max_nodes");
-  for (size_t i = 0; i < n; ++i) nodes[i] = reinterpret_cast<void*>(deps[i]);
-  *n_out = (int)n;
-  return JR_OK;
-}
-
-JR_API int jr_graph_set_deps(void* stream, void* const* nodes, int n) {
-  if (n < 0 || (n > 0 && !nodes)) return fail(JR_ERR_INVALID, "graph_set_deps: bad arguments");
-  const hipError_t e = hipStreamUpdateCaptureDependencies(
-      as_stream(stream), reinterpret_cast<hipGraphNode_t*>(const_cast<void**>(nodes)), (size_t)n,
-      hipStreamSetCaptureDependencies);
-  if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("graph_set_deps: ") + hipGetErrorString(e));
-  return JR_OK;
-}
-
 JR_API int jr_graph_launch(void* graph_exec, void* stream) {
   if (!graph_exec) return fail(JR_ERR_INVALID, "graph_launch: null graph");
   const hipError_t e = hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(graph_exec), as_stream(stream));

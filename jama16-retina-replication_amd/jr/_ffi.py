@@ -125,8 +125,6 @@ _SIGS = {
                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "jr_graph_begin": (c_int, [c_void_p]),
     "jr_graph_end": (c_int, [c_void_p, POINTER(c_void_p)]),
-    "jr_graph_get_deps": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
-    "jr_graph_set_deps": (c_int, [c_void_p, c_void_p, c_int]),
     "jr_graph_launch": (c_int, [c_void_p, c_void_p]),
     "jr_graph_destroy": (c_int, [c_void_p]),
 }

@@ -677,17 +677,18 @@ class Engine:
 
     def capture(self, B: Optional[int] = None) -> None:
         """Capture fwd+bwd+update for batch B into a HIP graph (single GPU;
-        not for Adam, whose step scalar changes every step);
-        the lanes become parallel branches of the graph.  Up to two lanes
-        the lane streams themselves are captured (fork/join by events: the
-        faster graph on ROCm 7.2); beyond that the DAG is built explicitly
-        on ONE capturing stream (capture_dag), because cross-waits among
-        three or more captured streams crashed hipGraphInstantiate."""
+        not for Adam, whose step scalar changes every step); the two lane
+        streams are captured (fork/join by events) and become parallel
+        branches of the graph.  At most two lanes: on ROCm 7.2, cross-waits
+        among three or more captured streams crashed hipGraphInstantiate, and
+        the same DAG built explicitly on one capturing stream (stream capture
+        dependencies set per call) crashed hipGraphLaunch depending on the
+        process's history; more lanes run eagerly."""
         B = B or self.batch
         if self.optimizer == "adam":
             raise ValueError("Adam steps run eagerly (the step's alpha is a host scalar)")
         if self.nlanes > 2:
-            return self.capture_dag(B)
+            raise ValueError("HIP graph capture supports at most two lanes (more lanes run eagerly)")
         fwd, bwd, opt, _, _ = self._build_calls(B)
         torch.cuda.synchronize(self.device)
         _ffi.check("jr_graph_begin", self.lib.jr_graph_begin(self._s))
@@ -701,45 +702,6 @@ class Engine:
         finally:
             ex = ctypes.c_void_p()
             _ffi.check("jr_graph_end", self.lib.jr_graph_end(self._s, ctypes.byref(ex)))
-        self._graphs[B] = ex.value
-
-    def capture_dag(self, B: Optional[int] = None) -> None:
-        """Graph capture with the lanes built explicitly on ONE capturing
-        stream: before each call the stream's capture dependencies are set
-        to its lane's tail plus the tails of the lanes it waits for
-        (jr.lanes.schedule), and the call's last node becomes its lane's new
-        tail."""
-        B = B or self.batch
-        fwd, bwd, opt, _, _ = self._build_calls(B, one_stream=True)
-        L = self.lib
-        torch.cuda.synchronize(self.device)
-        buf = (ctypes.c_void_p * 256)()
-        cnt = ctypes.c_int()
-
-        def get_deps():
-            _ffi.check("jr_graph_get_deps", L.jr_graph_get_deps(self._s, buf, 256, ctypes.byref(cnt)))
-            return [buf[i] for i in range(cnt.value)]
-
-        def set_deps(nodes):
-            arr = (ctypes.c_void_p * max(1, len(nodes)))(*nodes)
-            _ffi.check("jr_graph_set_deps", L.jr_graph_set_deps(self._s, arr, len(nodes)))
-
-        _ffi.check("jr_graph_begin", L.jr_graph_begin(self._s))
-        try:
-            start = get_deps()
-            tail = {ln: start for ln in range(self.nlanes)}
-            for c in fwd + bwd + opt:
-                if c.fn == "param_ready":
-                    continue
-                set_deps(list(dict.fromkeys(tail[c.lane] + [x for lj in c.waits for x in tail[lj]])))
-                rc = c.fn(*c.args)
-                if rc:
-                    raise _ffi.JRError(c.name, rc, _ffi.last_error())
-                tail[c.lane] = get_deps()
-            set_deps(list(dict.fromkeys(x for ln in sorted(tail) for x in tail[ln])))   # join
-        finally:
-            ex = ctypes.c_void_p()
-            _ffi.check("jr_graph_end", L.jr_graph_end(self._s, ctypes.byref(ex)))
         self._graphs[B] = ex.value
 
     def replay(self, B: Optional[int] = None) -> None:
@@ -760,9 +722,19 @@ class Engine:
         return self.probs[:B * self.units].cpu().numpy().reshape(B, self.units)
 
     def close(self) -> None:
-        for ex in self._graphs.values():
+        """Destroy this engine's HIP graph executables (also on collection)."""
+        graphs = getattr(self, "_graphs", None)
+        if not graphs:
+            return
+        for ex in graphs.values():
             self.lib.jr_graph_destroy(ctypes.c_void_p(ex))
-        self._graphs.clear()
+        graphs.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # interpreter shutdown: the library may be gone
+            pass
 
     def __del__(self):
         try:

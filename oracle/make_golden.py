@@ -10,7 +10,7 @@ vectors (oracle/__init__.py).  These fixtures freeze the oracle's own outputs
 Weights are NOT stored: they are regenerated from the seed by jr.init
 (numpy PCG64), inputs from jr.synth (PCG64(432 + i)).
 
-  python oracle/make_golden.py [--only ops,metrics,net107,net299,curve,net299b64,net587b2]
+  python oracle/make_golden.py [--only ops,metrics,net107,net299,curve,curve16,curve16bf,net299b64,net587b2]
 
 BASELINE-size fixtures (net299b64: configs 2-3 geometry, 299^2 B=64;
 net587b2: config 5 geometry, 587^2 B=2) hold the fp64 results AND the same
@@ -175,6 +175,15 @@ def main():
         curve["losses_fp32_cpu"] = _net(299, 16, 0, steps=100, cycle=32, dtype="float32")["losses"]
         np.savez_compressed(os.path.join(OUT, "loss_curve_res299_b16.npz"), **curve)
         print(f"curve16: {time.time() - t0:.0f}s", flush=True)
+    if "curve16bf" in todo:
+        # the same 100 steps by the oracle with bf16 storage emulated where the
+        # GPU bf16 path stores bf16 (an independent bf16 implementation): its
+        # gap to fp64 is the envelope the bf16 engine's curve is judged by
+        p = os.path.join(OUT, "loss_curve_res299_b16.npz")
+        curve = dict(np.load(p))
+        curve["losses_bf16emu"] = _net(299, 16, 0, steps=100, cycle=32, bf16=True)["losses"]
+        np.savez_compressed(p, **curve)
+        print(f"curve16bf: {time.time() - t0:.0f}s", flush=True)
     for key, res, batch in (("net299b64", 299, 64), ("net587b2", 587, 2)):
         if key in todo:
             d = _net(res, batch, 0, proj=True)

@@ -110,51 +110,6 @@ def test_partial_batch_uses_batch_statistics():
     assert np.max(np.abs(p - pr.numpy())) < 1e-4
 
 
-def test_bf16_loss_curve_tracks_f32():
-    """bf16 path (BASELINE configs 3 and 5): bf16 activations / filter copies,
-    fp32 MFMA accumulation, fp32 master weights, BN statistics, head and
-    optimizer.  Per-op parity is pinned teacher-forced in
-    test_gpu_layerwise.py; end to end a bf16 forward differs from fp32 by far
-    more than one rounding (this BN-heavy net amplifies a 2^-9 perturbation
-    up to ~10^3-fold at small BN populations; on random labels two fp32
-    implementations decorrelate within a few steps too), so the end-to-end
-    bar is the shape of the training trajectory at the full 299^2 geometry:
-    30 Nesterov steps on one fixed batch of 8 from the same weights, bf16 vs
-    the fp32 engine: the first 2 losses within 0.05, both fit the batch
-    (final loss < 0.3x initial) and cross half the initial loss at most 8
-    steps apart.  Both engines use the heuristic tile configs, so the curves
-    are bitwise reproducible on any MI355X (measured: first losses 0.014 /
-    0.025 apart, crossings at steps 20 (fp32) and 13 (bf16)); with autotuned
-    configs the summation order follows the box's timings and the second
-    loss alone moved by up to 0.05 between boxes."""
-    from jr.engine import Engine
-    from jr import synth
-    B, res = 8, 299
-    imgs = synth.fundus_batch(0, B, res)
-    y = np.array([[1.0], [0.0]] * 4, np.float32)
-    # heuristic tile configs, not autotuned ones: the autotuner picks by
-    # timing, so the summation order -- and, amplified by the BN layers, the
-    # second loss -- would depend on the box (0.05 bound crossed on one box)
-    eng = {dt: Engine(B, res, res, seed=5, dtype=dt, autotune=False) for dt in ("f32", "bf16")}
-    curves = {dt: [] for dt in eng}
-    for dt, e in eng.items():
-        e.set_batch(imgs, y)
-        for _ in range(30):
-            e.train_step()
-            curves[dt].append(e.loss_value())
-    f, h = np.array(curves["f32"]), np.array(curves["bf16"])
-    print("f32 ", np.round(f, 3))
-    print("bf16", np.round(h, 3))
-    assert np.all(np.isfinite(h))
-    # the first steps agree before rounding differences compound ...
-    assert np.all(np.abs(f[:2] - h[:2]) <= 0.05), (f[:2], h[:2])
-    # ... both fit the batch, and bf16 reaches half the initial loss within
-    # a few steps of fp32 (measured: 7 steps apart with the pinned configs)
-    assert f[-3:].mean() < 0.3 * f[0] and h[-3:].mean() < 0.3 * h[0], (f, h)
-    cf, ch = int(np.argmax(f < 0.5 * f[0])), int(np.argmax(h < 0.5 * h[0]))
-    assert abs(cf - ch) <= 8, (cf, ch, f, h)
-
-
 def test_bf16_graph_replay_and_training_descends():
     """bf16 whole-step HIP graph == eager bitwise, and 15 steps on one fixed
     batch drive the loss down (the optimizer sees the fp32 master weights and
@@ -212,8 +167,9 @@ def test_sibling_fusion_matches_unfused(dtype):
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_lanes_are_bitwise_single_stream(dtype):
     """Branch-level concurrency (jr.lanes): the engine's own call schedule
-    orders every conflicting pair across lanes, and 4 lanes (eager and as a
-    HIP graph) give bitwise the single-stream result over several steps."""
+    orders every conflicting pair across lanes, and 4 lanes (eager) and 2
+    lanes (eager and as a HIP graph) give bitwise the single-stream result
+    over several steps; graph capture refuses more than two lanes."""
     from jr.engine import Engine
     from jr.lanes import check_schedule
     from jr import synth
@@ -221,25 +177,26 @@ def test_lanes_are_bitwise_single_stream(dtype):
     y = np.array([[1.0], [0.0], [1.0], [0.0]], np.float32)
     one = Engine(4, 107, 107, seed=6, dtype=dtype, lanes=1)
     many = Engine(4, 107, 107, seed=6, dtype=dtype, lanes=4)
-    graph = Engine(4, 107, 107, seed=6, dtype=dtype, lanes=4)     # explicit-DAG capture
+    two = Engine(4, 107, 107, seed=6, dtype=dtype, lanes=2)
     graph2 = Engine(4, 107, 107, seed=6, dtype=dtype, lanes=2)    # two captured streams
     fwd, bwd, opt, _, _ = many._build_calls(4)
     seq = sorted([c for c in fwd + bwd + opt if c.idx >= 0], key=lambda c: c.idx)
     check_schedule(seq)
     assert len({c.lane for c in seq}) == 4
-    for e in (one, many, graph, graph2):
+    with pytest.raises(ValueError):
+        many.capture()
+    for e in (one, many, two, graph2):
         e.set_batch(imgs, y)
     # (tile choices are process-global in libjr: all four use the same ones)
-    graph.capture()
     graph2.capture()
     for _ in range(3):
         one.train_step()
         many.train_step()
-        graph.replay()
+        two.train_step()
         graph2.replay()
-    for e in (one, many, graph, graph2):
+    for e in (one, many, two, graph2):
         e.synchronize()
-    for e in (many, graph, graph2):
+    for e in (many, two, graph2):
         assert np.array_equal(one.params_numpy(), e.params_numpy())
         assert one.loss_value() == e.loss_value()
 
