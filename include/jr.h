@@ -161,6 +161,20 @@ int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t dy_c_str
                    int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c, const float* mean,
                    const float* invstd, const float* beta, void* dx, float* dbeta, void* ws, size_t ws_bytes,
                    void* stream);
+/* The same backward for the members of a fused sibling launch in ONE set of
+ * launches: x / dx / mean / invstd span the launch's c channels; segment i
+ * (channels [sum_{j<i} c_j, ... + c_i), sum c_i = c, each c_i a multiple of
+ * 4 fp32 / 8 bf16) brings its own upstream gradient slice and its own beta /
+ * dbeta.  1 <= nseg <= 4.  jr_bn_relu_bwd is the one-segment case. */
+typedef struct jr_bn_seg {
+  const void* dy;
+  int32_t dy_c_off, dy_c_stride, c;
+  const float* beta;
+  float* dbeta;
+} jr_bn_seg;
+int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
+                         int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd, void* dx,
+                         void* ws, size_t ws_bytes, void* stream);
 
 /* ---- pooling (Keras MaxPooling2D((3,3),(2,2)) / AveragePooling2D((3,3),
  *      (1,1),'same') inside InceptionV3, train.py:129-130) ------------ */

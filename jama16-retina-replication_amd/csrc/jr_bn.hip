@@ -95,6 +95,8 @@ static ChunkGeom chunk_geom(int64_t m, int c, int vw) {
 #ifndef JR_BN_MIN_ROWS
 #define JR_BN_MIN_ROWS 16
 #endif
+  // (round 2: a smaller minimum for small m only -- 4 rows per thread below
+  // 32,768 rows -- measured slower too: bf16 step 11.46 vs 11.35 ms)
   const int un = JR_BN_MIN_ROWS;
   int64_t rpc = std::max<int64_t>(ceil_div(m, kMaxChunks), (int64_t)rpp * un);
   rpc = ceil_div(rpc, (int64_t)rpp * un) * rpp * un;
@@ -104,6 +106,28 @@ static ChunkGeom chunk_geom(int64_t m, int c, int vw) {
   return g;
 }
 
+// Backward inputs of one launch over the c channels of a conv launch's raw
+// output: up to kMaxSegs channel segments (the members of a fused sibling
+// group, jr_bn_relu_bwd_multi), each with its own upstream gradient slice
+// and its own beta / dbeta (the members' tensors are separate).  A thread's
+// channel vector is fixed, so it resolves its segment once.
+constexpr int kMaxSegs = 4;
+struct BnSegs {
+  const void* dy[kMaxSegs];
+  const float* beta[kMaxSegs];
+  float* dbeta[kMaxSegs];
+  int dy_off[kMaxSegs], dy_stride[kMaxSegs];
+  int c0[kMaxSegs + 1];   // first channel of each segment; c0[n] = c
+  int n;
+};
+
+__device__ __forceinline__ int seg_of(const BnSegs& sg, int ch) {
+  int s = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxSegs; ++i) s += (i < sg.n && ch >= sg.c0[i]) ? 1 : 0;
+  return s;
+}
+
 // Per-chunk column sums.  MODE 0: (sum x, sum x^2).  MODE 1 (bwd):
 // (sum dy', sum dy'*xhat).  Per-thread fp64 sums over a fixed row set,
 // fixed-order block combine: deterministic.  Loads stay packed (one uint4
@@ -111,11 +135,9 @@ static ChunkGeom chunk_geom(int64_t m, int c, int vw) {
 // per thread: the loop is latency-bound, not bandwidth-bound, with fewer.
 // Partials: part[2][c][nchunks] (fp64, chunk-contiguous for the finalize).
 template <int MODE, typename T>
-__global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int xs, const T* __restrict__ dy,
-                                                   int dy_off, int dy_stride, int64_t m, int c,
+__global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int xs, BnSegs sg, int64_t m, int c,
                                                    int rows_per_chunk, const float* __restrict__ mean,
-                                                   const float* __restrict__ invstd,
-                                                   const float* __restrict__ beta, double* part) {
+                                                   const float* __restrict__ invstd, double* part) {
   constexpr int VW = Vec<T>::N;
   constexpr int U = red_rows<MODE>();
   __shared__ double red[256 * 2 * VW];
@@ -130,14 +152,18 @@ __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int 
   for (int j = 0; j < VW; ++j) s0[j] = s1[j] = 0.0;
   if (rr < rpp) {
     float mu[VW], is[VW], be[VW];
+    const T* gp = nullptr;
+    int dy_stride = 0;
     if (MODE == 1) {
+      const int sgi = seg_of(sg, q * VW), lc = q * VW - sg.c0[sgi];
+      gp = static_cast<const T*>(sg.dy[sgi]) + sg.dy_off[sgi] + lc;
+      dy_stride = sg.dy_stride[sgi];
 #pragma unroll
       for (int j = 0; j < VW; ++j) {
-        mu[j] = mean[q * VW + j]; is[j] = invstd[q * VW + j]; be[j] = beta[q * VW + j];
+        mu[j] = mean[q * VW + j]; is[j] = invstd[q * VW + j]; be[j] = sg.beta[sgi][lc + j];
       }
     }
     const T* xp = x + q * VW;
-    const T* gp = MODE == 1 ? dy + dy_off + q * VW : nullptr;
     for (int64_t r = r0 + rr; r < r1; r += (int64_t)rpp * U) {
       uint4 xr[U], gr[U];
 #pragma unroll
@@ -225,8 +251,7 @@ __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int 
 // MODE 0: mean, invstd.   MODE 1: k1 = sum dy'/m, k2 = sum dy'xhat/m, dbeta.
 template <int MODE>
 __global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ part, int nchunks, int c,
-                                                     int64_t m, float eps, float* out0, float* out1,
-                                                     float* dbeta) {
+                                                     int64_t m, float eps, float* out0, float* out1, BnSegs sg) {
   const int lane = threadIdx.x & 63;
   const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (k >= c) return;   // wave-uniform
@@ -257,7 +282,8 @@ __global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ 
   } else {
     out0[k] = (float)(s0 * inv_m);
     out1[k] = (float)(s1 * inv_m);
-    dbeta[k] = (float)s0;
+    const int sgi = seg_of(sg, k);
+    sg.dbeta[sgi][k - sg.c0[sgi]] = (float)s0;
   }
 }
 
@@ -299,11 +325,9 @@ __global__ void __launch_bounds__(256) k_bn_relu_apply(const T* __restrict__ x, 
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(const T* __restrict__ dy, int dy_off, int dy_stride,
-                                                           const T* __restrict__ x, int xs, int64_t m, int c,
-                                                           const float* __restrict__ mean,
+__global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(BnSegs sg, const T* __restrict__ x, int xs, int64_t m,
+                                                           int c, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
-                                                           const float* __restrict__ beta,
                                                            const float* __restrict__ k1,
                                                            const float* __restrict__ k2, T* dx) {
   constexpr int VW = Vec<T>::N;
@@ -312,11 +336,14 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(const T* __restrict__
   const int t = threadIdx.x;
   const int q = t % tpr, rr = t / tpr;
   if (rr >= rpp) return;
+  const int sgi = seg_of(sg, q * VW), lc = q * VW - sg.c0[sgi];
+  const T* dy = static_cast<const T*>(sg.dy[sgi]) + sg.dy_off[sgi] + lc;
+  const int dy_stride = sg.dy_stride[sgi];
   float mu[VW], is[VW], be[VW], c1[VW], c2[VW];
 #pragma unroll
   for (int j = 0; j < VW; ++j) {
     const int k = q * VW + j;
-    mu[j] = mean[k]; is[j] = invstd[k]; be[j] = beta[k]; c1[j] = k1[k]; c2[j] = k2[k];
+    mu[j] = mean[k]; is[j] = invstd[k]; be[j] = sg.beta[sgi][lc + j]; c1[j] = k1[k]; c2[j] = k2[k];
   }
   const int64_t r0 = (int64_t)blockIdx.x * rpp * kAppUnroll + rr;
   float xv[kAppUnroll][VW], gv[kAppUnroll][VW];
@@ -325,7 +352,7 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(const T* __restrict__
     const int64_t r = r0 + (int64_t)u * rpp;
     if (r < m) {
       Vec<T>::ld(x + r * xs + q * VW, xv[u]);
-      Vec<T>::ld(dy + r * dy_stride + dy_off + q * VW, gv[u]);
+      Vec<T>::ld(dy + r * dy_stride, gv[u]);
     }
   }
 #pragma unroll
@@ -389,17 +416,17 @@ JR_API int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps
   const ChunkGeom g = chunk_geom(m, c, vec_width(dtype));
   double* part = static_cast<double*>(ws);
   hipStream_t s = as_stream(stream);
+  const BnSegs none{};
   if (dtype == JR_F32)
-    hipLaunchKernelGGL((k_bn_reduce<0, float>), dim3(g.nchunks), dim3(256), 0, s, (const float*)x, c,
-                       (const float*)nullptr, 0, 0, m, c, g.rows_per_chunk, nullptr, nullptr, nullptr, part);
+    hipLaunchKernelGGL((k_bn_reduce<0, float>), dim3(g.nchunks), dim3(256), 0, s, (const float*)x, c, none, m, c,
+                       g.rows_per_chunk, nullptr, nullptr, part);
   else
-    hipLaunchKernelGGL((k_bn_reduce<0, uint16_t>), dim3(g.nchunks), dim3(256), 0, s, (const uint16_t*)x, c,
-                       (const uint16_t*)nullptr, 0, 0, m, c, g.rows_per_chunk, nullptr, nullptr, nullptr,
-                       part);
+    hipLaunchKernelGGL((k_bn_reduce<0, uint16_t>), dim3(g.nchunks), dim3(256), 0, s, (const uint16_t*)x, c, none,
+                       m, c, g.rows_per_chunk, nullptr, nullptr, part);
   rc = check_launch("bn_stats reduce");
   if (rc) return rc;
   hipLaunchKernelGGL((k_bn_finalize<0>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, g.nchunks, c, m,
-                     eps, mean, invstd, (float*)nullptr);
+                     eps, mean, invstd, none);
   return check_launch("bn_stats finalize");
 }
 
@@ -424,47 +451,75 @@ JR_API int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x
   return check_launch("bn_relu_apply");
 }
 
-JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t dy_c_stride, const void* x,
-                          int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c, const float* mean,
-                          const float* invstd, const float* beta, void* dx, float* dbeta, void* ws, size_t ws_bytes,
-                          void* stream) {
-  int rc = check_common(dtype, m, c);
-  if (rc) return rc;
-  if (!dy || !x || !mean || !invstd || !beta || !dx || !dbeta)
-    return fail(JR_ERR_INVALID, "bn_relu_bwd: null pointer");
-  if (!check_slice(dtype, x_c_off, x_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_bwd: bad x / dx slice");
-  const size_t esz = dtype == JR_BF16 ? 2 : 4;
-  x = static_cast<const char*>(x) + (size_t)x_c_off * esz;
-  dx = static_cast<char*>(dx) + (size_t)x_c_off * esz;
-  if (!check_slice(dtype, dy_c_off, dy_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_bwd: bad dy slice");
+// The three backward launches over segments (validated by the callers).
+static int bn_bwd_launch(int dtype, const BnSegs& sg, const void* x, int32_t x_c_stride, int64_t m, int32_t c,
+                         const float* mean, const float* invstd, void* dx, void* ws, size_t ws_bytes,
+                         hipStream_t s) {
   if (!ws || ws_bytes < ws_need(m, c)) return fail(JR_ERR_WORKSPACE, "bn_relu_bwd: workspace too small");
   const int vw = vec_width(dtype);
   const ChunkGeom g = chunk_geom(m, c, vw);
   double* part = static_cast<double*>(ws);
   float* k1 = reinterpret_cast<float*>(part + (size_t)g.nchunks * 2 * c);
   float* k2 = k1 + c;
-  hipStream_t s = as_stream(stream);
   if (dtype == JR_F32)
-    hipLaunchKernelGGL((k_bn_reduce<1, float>), dim3(g.nchunks), dim3(256), 0, s, (const float*)x, x_c_stride,
-                       (const float*)dy, dy_c_off, dy_c_stride, m, c, g.rows_per_chunk, mean, invstd, beta,
-                       part);
+    hipLaunchKernelGGL((k_bn_reduce<1, float>), dim3(g.nchunks), dim3(256), 0, s, (const float*)x, x_c_stride, sg,
+                       m, c, g.rows_per_chunk, mean, invstd, part);
   else
     hipLaunchKernelGGL((k_bn_reduce<1, uint16_t>), dim3(g.nchunks), dim3(256), 0, s, (const uint16_t*)x,
-                       x_c_stride, (const uint16_t*)dy, dy_c_off, dy_c_stride, m, c, g.rows_per_chunk, mean, invstd,
-                       beta, part);
-  rc = check_launch("bn_bwd reduce");
+                       x_c_stride, sg, m, c, g.rows_per_chunk, mean, invstd, part);
+  int rc = check_launch("bn_bwd reduce");
   if (rc) return rc;
-  hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, g.nchunks, c, m,
-                     0.f, k1, k2, dbeta);
+  hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, g.nchunks, c, m, 0.f,
+                     k1, k2, sg);
   rc = check_launch("bn_bwd finalize");
   if (rc) return rc;
   const int grid = apply_grid(m, c, vw);
   if (dtype == JR_F32)
-    hipLaunchKernelGGL(k_bn_relu_bwd_apply<float>, dim3(grid), dim3(256), 0, s, (const float*)dy, dy_c_off,
-                       dy_c_stride, (const float*)x, x_c_stride, m, c, mean, invstd, beta, k1, k2, (float*)dx);
+    hipLaunchKernelGGL(k_bn_relu_bwd_apply<float>, dim3(grid), dim3(256), 0, s, sg, (const float*)x, x_c_stride, m,
+                       c, mean, invstd, k1, k2, (float*)dx);
   else
-    hipLaunchKernelGGL(k_bn_relu_bwd_apply<uint16_t>, dim3(grid), dim3(256), 0, s, (const uint16_t*)dy,
-                       dy_c_off, dy_c_stride, (const uint16_t*)x, x_c_stride, m, c, mean, invstd, beta, k1, k2,
-                       (uint16_t*)dx);
+    hipLaunchKernelGGL(k_bn_relu_bwd_apply<uint16_t>, dim3(grid), dim3(256), 0, s, sg, (const uint16_t*)x,
+                       x_c_stride, m, c, mean, invstd, k1, k2, (uint16_t*)dx);
   return check_launch("bn_bwd apply");
+}
+
+JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t dy_c_stride, const void* x,
+                          int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c, const float* mean,
+                          const float* invstd, const float* beta, void* dx, float* dbeta, void* ws, size_t ws_bytes,
+                          void* stream) {
+  jr_bn_seg seg{dy, dy_c_off, dy_c_stride, c, beta, dbeta};
+  return jr_bn_relu_bwd_multi(dtype, 1, &seg, x, x_c_off, x_c_stride, m, c, mean, invstd, dx, ws, ws_bytes, stream);
+}
+
+JR_API int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
+                                int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd,
+                                void* dx, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_common(dtype, m, c);
+  if (rc) return rc;
+  if (!segs || nseg < 1 || nseg > kMaxSegs) return fail(JR_ERR_INVALID, "bn_relu_bwd: 1..4 segments");
+  if (!x || !mean || !invstd || !dx) return fail(JR_ERR_INVALID, "bn_relu_bwd: null pointer");
+  if (!check_slice(dtype, x_c_off, x_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_bwd: bad x / dx slice");
+  const size_t esz = dtype == JR_BF16 ? 2 : 4;
+  BnSegs sg{};
+  sg.n = nseg;
+  int c0 = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const jr_bn_seg& e = segs[i];
+    if (!e.dy || !e.beta || !e.dbeta) return fail(JR_ERR_INVALID, "bn_relu_bwd: null pointer in a segment");
+    if (e.c <= 0 || e.c % vec_width(dtype) != 0)
+      return fail(JR_ERR_INVALID, "bn_relu_bwd: segment channels must be a positive multiple of 4 (fp32) / 8 (bf16)");
+    if (!check_slice(dtype, e.dy_c_off, e.dy_c_stride, e.c)) return fail(JR_ERR_INVALID, "bn_relu_bwd: bad dy slice");
+    sg.dy[i] = e.dy;
+    sg.dy_off[i] = e.dy_c_off;
+    sg.dy_stride[i] = e.dy_c_stride;
+    sg.beta[i] = e.beta;
+    sg.dbeta[i] = e.dbeta;
+    sg.c0[i] = c0;
+    c0 += e.c;
+  }
+  if (c0 != c) return fail(JR_ERR_INVALID, "bn_relu_bwd: segment channels must sum to c");
+  sg.c0[nseg] = c;
+  x = static_cast<const char*>(x) + (size_t)x_c_off * esz;
+  dx = static_cast<char*>(dx) + (size_t)x_c_off * esz;
+  return bn_bwd_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, dx, ws, ws_bytes, as_stream(stream));
 }

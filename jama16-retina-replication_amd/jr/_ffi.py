@@ -44,6 +44,12 @@ class WPrep(Structure):
                 ("reserved", c_int32)]
 
 
+class BnSeg(Structure):
+    """include/jr.h jr_bn_seg: one member's upstream gradient slice and beta / dbeta."""
+    _fields_ = [("dy", c_void_p), ("dy_c_off", c_int32), ("dy_c_stride", c_int32), ("c", c_int32),
+                ("beta", c_void_p), ("dbeta", c_void_p)]
+
+
 class PoolDesc(Structure):
     _fields_ = [(n, c_int32) for n in (
         "n", "h", "w", "c", "ho", "wo", "x_c_off", "x_c_stride", "y_c_off", "y_c_stride")]
@@ -94,6 +100,8 @@ _SIGS = {
     "jr_bn_relu_bwd": (c_int, [c_int, c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_size_t, c_void_p]),
+    "jr_bn_relu_bwd_multi": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int32,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "jr_maxpool3x3s2_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p,
                                     c_void_p]),
     "jr_maxpool3x3s2_bwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p, c_int,

@@ -201,8 +201,7 @@ class Engine:
             ops = (_ffi.JR_CONV_FWD, _ffi.JR_CONV_BWD_DATA, _ffi.JR_CONV_BWD_FILTER)
             for op in (ops if self.train_mode else ops[:1]):
                 ws = max(ws, self.lib.jr_conv2d_workspace_size(ctypes.byref(d), op, self.cdt))
-            for n in u.members:
-                ws = max(ws, self.lib.jr_bn_workspace_size(B * n.ho * n.wo, n.cout))
+            ws = max(ws, self.lib.jr_bn_workspace_size(B * u.ho * u.wo, u.cout))   # one backward per launch (or less)
         self.ws_bytes = int(ws)
         self.ws_lane = [self._t((self.ws_bytes + 15) // 4 + 4) for _ in range(self.nlanes)]
         self.ws = self.ws_lane[0]
@@ -517,14 +516,27 @@ class Engine:
                     uid = u.first.idx
                     raw = self.raw_unit[uid].data_ptr()
                     draw = self.draw_lane[ln].data_ptr()
-                    for m, co in zip(u.members, u.col_off):
-                        yb = g.bufs[m.y.buf]
-                        add(bwd, L.jr_bn_relu_bwd, (dt, D(m.y.buf), m.y.c_off, yb.c, raw, co, u.cout, M, m.cout,
-                                                    self.mean[m.idx].data_ptr(), self.invstd[m.idx].data_ptr(),
-                                                    self._p(f"batch_normalization_{m.idx + 1}/beta"), draw,
-                                                    self._gp(f"batch_normalization_{m.idx + 1}/beta"), ws, wsb, s),
-                            "bn_relu_bwd", ln, [("d", m.y.buf, m.y.c_off), ("r", uid), ("p",)],
-                            [("draw", ln), ("g", uid), ("ws", ln)], nbytes=3 * M * m.cout * self.esz)
+                    # one backward launch set for all members of the launch (segments:
+                    # each member's upstream gradient slice, beta and dbeta) while the
+                    # launch's channels fit one 256-thread row (jr_bn: <= 256 vectors of
+                    # 4 fp32 / 8 bf16); else one set per member
+                    groups = [list(zip(u.members, u.col_off))]
+                    if u.cout // (8 if dt == _ffi.JR_BF16 else 4) > 256:
+                        groups = [[mc] for mc in groups[0]]
+                    for grp in groups:
+                        co0 = grp[0][1]
+                        cg = sum(m.cout for m, _ in grp)
+                        segs = (_ffi.BnSeg * len(grp))(*[
+                            _ffi.BnSeg(D(m.y.buf), m.y.c_off, g.bufs[m.y.buf].c, m.cout,
+                                       self._p(f"batch_normalization_{m.idx + 1}/beta"),
+                                       self._gp(f"batch_normalization_{m.idx + 1}/beta")) for m, _ in grp])
+                        keep.append(segs)
+                        add(bwd, L.jr_bn_relu_bwd_multi, (dt, len(grp), ctypes.byref(segs), raw, co0, u.cout, M, cg,
+                                                          self.mean_unit[uid].data_ptr() + 4 * co0,
+                                                          self.invstd_unit[uid].data_ptr() + 4 * co0, draw, ws, wsb,
+                                                          s),
+                            "bn_relu_bwd", ln, [("d", m.y.buf, m.y.c_off) for m, _ in grp] + [("r", uid), ("p",)],
+                            [("draw", ln), ("g", uid), ("ws", ln)], nbytes=3 * M * cg * self.esz)
                     dkey = ("draw", ln)
                     if x8p:             # the raw-output gradient as split planes (dgrad and wgrad operand)
                         drawp = self.drawp_lane[ln].data_ptr()

@@ -138,8 +138,10 @@ def test_engine_optimizer_step(opt):
     for t in (1, 2):
         eng.forward()
         eng.backward()
+        eng.synchronize()            # the engine's lane streams, not torch's current stream
         g = eng.grads.cpu().numpy().copy()
         eng.apply_update()
+        eng.synchronize()
         if opt == "adam":
             w, m, v, _ = R.adam_f32(w, g, m, v, t, lr=1e-3)
         else:

@@ -439,3 +439,69 @@ def test_u8_scale_is_tf_convert_image_dtype():
     out = torch.zeros(256, device="cuda")
     ffi.check("u8", L.jr_u8_to_f32_scaled(dev(u8, torch.uint8).data_ptr(), out.data_ptr(), 0, 256, None))
     assert np.array_equal(host(out), R.convert_image_dtype_u8(u8))
+
+
+@pytest.mark.parametrize("dt", [0, 1], ids=["f32", "bf16"])
+def test_bn_relu_bwd_multi_segments(dt):
+    """jr_bn_relu_bwd_multi: one backward launch set for the members of a
+    fused sibling launch (raw output [m][48+64+96], each member's upstream
+    gradient a slice of its own wider buffer, its own beta / dbeta) equals
+    the three per-member jr_bn_relu_bwd calls (the fp64 partial grouping
+    differs with the channel count: within 1e-6 fp32 / one bf16 ulp) and, in
+    fp32, the fp64 oracle."""
+    ffi = _lib()
+    L = ffi.load()
+    m, cs = 64 * 17 * 17, (48, 64, 96)
+    c = sum(cs)
+    tdt = torch.float32 if dt == 0 else torch.bfloat16
+    rng = np.random.default_rng(11)
+    x = (rng.standard_normal((m, c)) * 2 + rng.standard_normal(c)).astype(np.float32)
+    X = torch.as_tensor(x).to(tdt).cuda()
+    xs = X.float()
+    MEAN = xs.double().mean(0).float()
+    INV = (1.0 / torch.sqrt(xs.double().var(0, unbiased=False) + 1e-3)).float()
+    dys, betas, offs, strides = [], [], (8, 0, 16), (cs[0] + 16, cs[1], cs[2] + 24)
+    for k, ck in enumerate(cs):
+        buf = torch.zeros((m, strides[k]), dtype=tdt, device="cuda")
+        buf[:, offs[k]:offs[k] + ck] = torch.as_tensor(rng.standard_normal((m, ck)).astype(np.float32)).to(tdt)
+        dys.append(buf)
+        betas.append(torch.as_tensor((rng.standard_normal(ck) * 0.5).astype(np.float32)).cuda())
+    wsb = L.jr_bn_workspace_size(m, c)
+    ws = torch.zeros(wsb // 4 + 4, device="cuda")
+    DB = [torch.zeros(ck, device="cuda") for ck in cs]
+    DX = torch.full((m, c), 7.0, dtype=tdt, device="cuda")
+    segs = (ffi.BnSeg * 3)(*[ffi.BnSeg(dys[k].data_ptr(), offs[k], strides[k], cs[k], betas[k].data_ptr(),
+                                       DB[k].data_ptr()) for k in range(3)])
+    ffi.check("multi", L.jr_bn_relu_bwd_multi(dt, 3, ctypes.byref(segs), X.data_ptr(), 0, c, m, c,
+                                               MEAN.data_ptr(), INV.data_ptr(), DX.data_ptr(), ws.data_ptr(), wsb,
+                                               None))
+    # per member: the member's slice of x / dx / mean / invstd
+    DX1 = torch.full((m, c), 7.0, dtype=tdt, device="cuda")
+    DB1 = [torch.zeros(ck, device="cuda") for ck in cs]
+    c0 = 0
+    esz = 4 if dt == 0 else 2
+    for k, ck in enumerate(cs):
+        ffi.check("single", L.jr_bn_relu_bwd(dt, dys[k].data_ptr(), offs[k], strides[k], X.data_ptr(), c0, c, m, ck,
+                                              MEAN.data_ptr() + 4 * c0, INV.data_ptr() + 4 * c0,
+                                              betas[k].data_ptr(), DX1.data_ptr(), DB1[k].data_ptr(),
+                                              ws.data_ptr(), wsb, None))
+        c0 += ck
+    torch.cuda.synchronize()
+    d0, d1 = DX1.float().cpu().numpy(), DX.float().cpu().numpy()
+    for k in range(3):
+        assert relerr(DB[k].cpu().numpy(), DB1[k].cpu().numpy()) <= 1e-6
+    if dt == 0:
+        assert relerr(d1, d0) <= 1e-6
+        beta = np.concatenate([b.cpu().numpy() for b in betas])
+        dy = np.concatenate([dys[k][:, offs[k]:offs[k] + cs[k]].cpu().numpy() for k in range(3)], axis=1)
+        pre = (x - MEAN.cpu().numpy()) * INV.cpu().numpy() + beta
+        dx_ref, db_ref = R.bn_relu_bwd(dy, x, beta, mask=pre > 0)
+        assert relerr(d1, dx_ref) < 1e-4
+        assert relerr(np.concatenate([b.cpu().numpy() for b in DB]), db_ref) < 1e-5
+    else:
+        assert np.all(np.abs(d1 - d0) <= np.abs(d0) * 2.0 ** -7 + 1e-30)
+    # validation: segments must sum to c
+    segs[2].c = 88
+    assert L.jr_bn_relu_bwd_multi(dt, 3, ctypes.byref(segs), X.data_ptr(), 0, c, m, c, MEAN.data_ptr(),
+                                  INV.data_ptr(), DX.data_ptr(), ws.data_ptr(), wsb, None) == -1
+    assert "sum to c" in ffi.last_error()
