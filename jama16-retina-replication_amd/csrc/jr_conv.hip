@@ -1020,7 +1020,14 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
       if (hipEventSynchronize(e1) != hipSuccess) { rc = fail(JR_ERR_HIP, "autotune: event sync failed"); return 1e30f; }
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, e0, e1);
-      if (ms < best_t) { best_t = ms; best_c = c; }
+      // near-ties go to the plan with fewer split-K slab bytes (fp32 partials
+      // written and re-read through HBM, which a back-to-back timing on a hot
+      // L2 undercounts): more splits must win by 2 %, fewer may lose by 2 %
+      const int ps = pc.splits > 1 ? pc.splits : 0;
+      const int bs = best_t < 1e29f ? (plan_with(dtype, best_c, M, N, K).splits > 1
+                                           ? plan_with(dtype, best_c, M, N, K).splits : 0) : 0;
+      const float bar = ps > bs ? 0.98f : ps < bs ? 1.02f : 1.0f;
+      if (ms < best_t * bar) { best_t = ms; best_c = c; }
       return ms;
     };
     // pass 1: every tile with the planner's split-K factor
