@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=64)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-defer-wgrad", action="store_true",
+                    help="reduce each split-K filter gradient right after its GEMM (A/B of jr_wgrad_reduce)")
     return ap.parse_args()
 
 
@@ -73,7 +75,7 @@ def conv_roofline(eng, steps: int = 3):
     bracket every conv fwd/dgrad/wgrad call; returns (flops/step, conv s/step)."""
     from jr import _ffi
     fwd, bwd, opt, _, _ = eng._build_calls(eng.batch, 1)     # one lane: calls do not overlap
-    conv_names = {"conv_fwd", "conv_dgrad", "conv_wgrad"}
+    conv_names = {"conv_fwd", "conv_dgrad", "conv_wgrad", "wgrad_reduce"}
     flops = 0
     for n in eng.g.convs:
         m = n.macs_per_image() * eng.batch
@@ -257,7 +259,7 @@ def main():
     B, res = args.batch or (64 if train else 32), args.res
     math = args.conv_math if args.dtype == "f32" else "bf16"
     eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0, lanes=args.lanes, train=train,
-                 conv_math=math, tiles=args.tiles)
+                 conv_math=math, tiles=args.tiles, defer_wgrad=not args.no_defer_wgrad)
     imgs = synth.fundus_batch(rank * B, B, res)
     labels = synth.labels(rank * B, B)
     eng.set_batch(imgs, labels)

@@ -127,6 +127,25 @@ int jr_conv2d_bwd_data(const jr_conv_desc* d, int dtype, const void* dy, const v
 int jr_conv2d_bwd_filter(const jr_conv_desc* d, int dtype, const void* x, const void* dy, float* dw,
                          void* ws, size_t ws_bytes, void* stream);
 
+/* Deferred filter-gradient reduce (one launch for many layers).  When the
+ * planned bwd_filter GEMM of a layer splits K (jr_conv2d_wgrad_seg: splits
+ * > 1), jr_conv2d_bwd_filter_slabs writes its fp32 partial slabs
+ * [splits][m][n] (splits * m * n * 4 bytes) into caller memory and returns;
+ * jr_wgrad_reduce later sums the slabs of every listed layer into its dw in
+ * ONE launch, bitwise equal to jr_conv2d_bwd_filter's own reduce.  segs is
+ * a DEVICE array; each entry is filled by jr_conv2d_wgrad_seg (geometry,
+ * lanes g, blocks) plus the caller's slabs / dw pointers and block0 = the
+ * exclusive prefix sum of blocks (total_blocks = the sum). */
+typedef struct jr_wgrad_seg {
+  const float* slabs;
+  float* dw;
+  int32_t m, n, splits, c_in, c_pad, g, block0, blocks;
+} jr_wgrad_seg;
+int jr_conv2d_wgrad_seg(const jr_conv_desc* d, int dtype, jr_wgrad_seg* seg);
+int jr_conv2d_bwd_filter_slabs(const jr_conv_desc* d, int dtype, const void* x, const void* dy, float* slabs,
+                               size_t slab_bytes, void* stream);
+int jr_wgrad_reduce(const jr_wgrad_seg* segs, int32_t nseg, int32_t total_blocks, void* stream);
+
 /* Time every candidate tile configuration of this op on the given buffers
  * (the output buffer is overwritten; host-synchronising) and cache the
  * fastest for later calls with the same geometry in this process.  Call

@@ -130,11 +130,14 @@ __device__ __forceinline__ int seg_of(const BnSegs& sg, int ch) {
 
 // Per-chunk column sums.  MODE 0: (sum x, sum x^2).  MODE 1 (bwd):
 // (sum dy', sum dy'*xhat).  Per-thread fp64 sums over a fixed row set,
-// fixed-order block combine: deterministic.  MODE 1 sums each batch of U
-// rows in fp32 (fma for dy'*xhat) and adds the batch sums in fp64: the
-// per-element fp64 conversions and adds had made the bf16 reduce
-// VALU-bound (bf16 step 11.22 -> 10.84 ms, fp32 26.94 -> 26.87 ms,
-// interleaved A/B on one box; per-shape bnbench: bf16 2.65 -> 2.16 ms).  Loads stay packed (one uint4
+// fixed-order block combine: deterministic.  bf16 MODE 1 sums each batch of
+// U rows in fp32 (fma for dy'*xhat) and adds the batch sums in fp64: the
+// per-element fp64 conversions and adds of 8 channels per thread had made
+// the bf16 reduce VALU-bound (bf16 step 11.22 -> 10.84 ms, interleaved A/B
+// on one box; per-shape bnbench 2.65 -> 2.16 ms).  fp32 (4 channels per
+// thread) gained 0.3 % from the same change and keeps per-element fp64 sums:
+// its 100-step loss-curve fixture is a chaotic trajectory that any change
+// of summation order moves past the per-step bar.  Loads stay packed (one uint4
 // per row and operand) until used, so red_rows<MODE>() rows are in flight
 // per thread: the loop is latency-bound, not bandwidth-bound, with fewer.
 // Partials: part[2][c][nchunks] (fp64, chunk-contiguous for the finalize).
@@ -154,7 +157,8 @@ __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int 
   double s0[VW], s1[VW];
 #pragma unroll
   for (int j = 0; j < VW; ++j) s0[j] = s1[j] = 0.0;
-  float f0[VW], f1[VW];   // MODE 1: fp32 sums of one batch of U rows
+  constexpr bool kBatch32 = sizeof(T) == 2;   // bf16: fp32 sums of one batch of U rows
+  float f0[VW], f1[VW];
 #pragma unroll
   for (int j = 0; j < VW; ++j) f0[j] = f1[j] = 0.f;
   if (rr < rpp) {
@@ -217,12 +221,17 @@ __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int 
             const float xh = bn_xhat(xv[j], mu[j], is[j]);
             const float pre = __fadd_rn(xh, be[j]);
             const float g = pre > 0.f ? gv[j] : 0.f;
-            f0[j] += g;
-            f1[j] = fmaf(g, xh, f1[j]);
+            if constexpr (kBatch32) {
+              f0[j] += g;
+              f1[j] = fmaf(g, xh, f1[j]);
+            } else {
+              s0[j] += (double)g;
+              s1[j] += (double)g * (double)xh;
+            }
           }
         }
       }
-      if (MODE == 1) {
+      if (MODE == 1 && kBatch32) {
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
           s0[j] += (double)f0[j];

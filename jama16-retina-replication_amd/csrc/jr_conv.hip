@@ -699,6 +699,15 @@ static Plan make_plan(int dtype, int op, int M, int N, int K, const jr_conv_desc
   return plan_with(dtype, cfg, M, N, K);
 }
 
+// z-lanes per float4 column of the split-K reduce (k_splitk_reduce and the
+// deferred k_wgrad_reduce: the same G gives the same summation order)
+static int reduce_lanes(const Plan& p) {
+  const long long total = (long long)p.M * p.N / 4;
+  int G = 1;
+  while (G < 64 && G * 4 <= p.splits && total * G < 128 * 1024) G *= 2;
+  return G;
+}
+
 static size_t plan_ws(const Plan& p) {
   return p.splits > 1 ? (size_t)p.splits * (size_t)p.M * (size_t)p.N * sizeof(float) : 0;
 }
@@ -814,9 +823,11 @@ static void fill_common(ConvArgs& a, const jr_conv_desc* d, int dtype) {
 }
 
 // One GEMM (plus its split-K reduce) on the stream.
+// defer (WGRAD): write the split-K slabs into ws and stop (jr_wgrad_reduce
+// sums them later, batched with other layers').
 template <int OP>
 static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, size_t ws_bytes, hipStream_t s,
-                    const StatsReq* st = nullptr) {
+                    const StatsReq* st = nullptr, bool defer = false) {
   if (p.M <= 0 || p.N <= 0) return JR_OK;
   int sP = 0, sR = 0;
   if (st) {
@@ -876,10 +887,9 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     }
     return check_launch("conv stats finalize");
   }
-  if (p.splits <= 1) return rc;
+  if (p.splits <= 1 || defer) return rc;
   const long long total = (long long)p.M * p.N / 4;   // float4 columns
-  int G = 1;                                            // z-lanes per column
-  while (G < 64 && G * 4 <= p.splits && total * G < 128 * 1024) G *= 2;
+  const int G = reduce_lanes(p);                       // z-lanes per column
   const long long cols = 256 / G;
   const int blocks = (int)std::min<long long>(ceil_div(total, cols), 8192);
   if (dtype == JR_BF16 && OP != OP_WGRAD)   // bf16 activations / activation grads; dW stays fp32
@@ -1120,9 +1130,103 @@ __global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict_
   }
 }
 
+// Deferred filter-gradient split-K reduce: ONE launch for the slabs of many
+// layers (jr_wgrad_reduce).  Block b belongs to the segment with the largest
+// block0 <= b and sums `256 / G` float4 columns of it exactly as
+// k_splitk_reduce does (z-lane zg adds slabs zg, zg + G, ... in order, the G
+// lane sums are added in zg order), so the result is bitwise that of the
+// per-layer reduce; only the launch count changes (75 -> 1 per step).
+__global__ void __launch_bounds__(256) k_wgrad_reduce(const jr_wgrad_seg* __restrict__ segs, int nseg) {
+  __shared__ float4 part[256];
+  const int b = blockIdx.x;
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {   // wave-uniform
+    const int mid = (lo + hi + 1) >> 1;
+    if (segs[mid].block0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const jr_wgrad_seg sg = segs[lo];
+  const int G = sg.g, cols = 256 / G;
+  const int t = threadIdx.x;
+  const int zg = t / cols, cl = t - zg * cols;
+  const int n4 = sg.n >> 2;
+  const long long total = (long long)sg.m * n4;   // = one slab, in float4
+  const long long e = (long long)(b - sg.block0) * cols + cl;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < total) {
+    const float4* src = reinterpret_cast<const float4*>(sg.slabs) + e;
+    for (int z = zg; z < sg.splits; z += G) {
+      const float4 a = src[z * total];
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+  }
+  if (G > 1) {
+    part[t] = s;
+    __syncthreads();
+    if (zg == 0) {
+      for (int k = 1; k < G; ++k) {
+        const float4 a = part[k * cols + cl];
+        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+      }
+    }
+  }
+  if (zg != 0 || e >= total) return;
+  const int m = (int)(e / n4), q = (int)(e - (long long)m * n4);
+  long long base = (long long)m * sg.n;            // out_row<OP_WGRAD>
+  if (sg.c_pad != sg.c_in) {
+    const int rc = m / sg.c_pad, ci = m - rc * sg.c_pad;
+    if (ci >= sg.c_in) return;
+    base = ((long long)rc * sg.c_in + ci) * sg.n;
+  }
+  *reinterpret_cast<float4*>(sg.dw + base + q * 4) = s;
+}
+
 }  // namespace jr
 
 using namespace jr;
+
+JR_API int jr_conv2d_wgrad_seg(const jr_conv_desc* d, int dtype, jr_wgrad_seg* seg) {
+  int rc = validate(d, OP_WGRAD, dtype);
+  if (rc) return rc;
+  if (!seg) return fail(JR_ERR_INVALID, "wgrad_seg: null segment");
+  const Plan p = plan_for(d, OP_WGRAD, dtype, nullptr);
+  seg->m = p.M;
+  seg->n = p.N;
+  seg->splits = p.splits;
+  seg->c_in = d->c_in;
+  seg->c_pad = chan_pad(d->c_in, dtype);
+  seg->g = reduce_lanes(p);
+  seg->block0 = 0;
+  seg->blocks = (int32_t)ceil_div((long long)p.M * p.N / 4, (long long)(256 / seg->g));
+  return JR_OK;
+}
+
+JR_API int jr_conv2d_bwd_filter_slabs(const jr_conv_desc* d, int dtype, const void* x, const void* dy, float* slabs,
+                                      size_t slab_bytes, void* stream) {
+  int rc = validate(d, OP_WGRAD, dtype);
+  if (rc) return rc;
+  if (!x || !dy || !slabs) return fail(JR_ERR_INVALID, "bwd_filter_slabs: null tensor pointer");
+  if (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)slabs) & 15)
+    return fail(JR_ERR_INVALID, "bwd_filter_slabs: tensors must be 16-byte aligned");
+  const Plan p = plan_for(d, OP_WGRAD, dtype, nullptr);
+  if (p.splits <= 1) return fail(JR_ERR_INVALID, "bwd_filter_slabs: the plan has no split-K (use jr_conv2d_bwd_filter)");
+  if (slab_bytes < plan_ws(p)) return fail(JR_ERR_WORKSPACE, "bwd_filter_slabs: slab buffer too small for the plan");
+  ConvArgs a{};
+  fill_common(a, d, dtype);
+  a.A = static_cast<const float*>(x);
+  a.B = static_cast<const float*>(dy);
+  if (dtype == JR_F32_X8P) {
+    a.a_ps = (long long)d->n * d->h * d->w * d->x_c_stride;
+    a.b_ps = (long long)d->n * d->ho * d->wo * d->y_c_stride;
+  }
+  a.c_off = 0; a.c_stride = d->c_out;
+  return run_gemm<OP_WGRAD>(dtype, a, p, nullptr, slabs, slab_bytes, as_stream(stream), nullptr, true);
+}
+
+JR_API int jr_wgrad_reduce(const jr_wgrad_seg* segs, int32_t nseg, int32_t total_blocks, void* stream) {
+  if (!segs || nseg <= 0 || total_blocks <= 0) return fail(JR_ERR_INVALID, "wgrad_reduce: empty segment table");
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(total_blocks), dim3(256), 0, as_stream(stream), segs, nseg);
+  return check_launch("wgrad_reduce");
+}
 
 JR_API int jr_conv2d_fwd_bn_stats(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y, float eps,
                                   float* mean, float* invstd, void* ws, size_t ws_bytes, void* stream) {

@@ -419,7 +419,7 @@ static void launch_tile(bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) 
 
 template <int OP, int NP>
 static void launch_op_bf16(int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  static_assert(kNumCfgsBf16 == 14 && kNumCfgsX8P == 14, "keep the switch in sync with kCfgsBf16 / kCfgsX8P");
+  static_assert(kNumCfgsBf16 == 17 && kNumCfgsX8P == 17, "keep the switch in sync with kCfgsBf16 / kCfgsX8P");
   switch (tile) {
     case 0: launch_tile<OP, 0, NP>(fast, a, grid, s); break;
     case 1: launch_tile<OP, 1, NP>(fast, a, grid, s); break;
@@ -434,7 +434,10 @@ static void launch_op_bf16(int tile, bool fast, const ConvArgs& a, dim3 grid, hi
     case 10: launch_tile<OP, 10, NP>(fast, a, grid, s); break;
     case 11: launch_tile<OP, 11, NP>(fast, a, grid, s); break;
     case 12: launch_tile<OP, 12, NP>(fast, a, grid, s); break;
-    default: launch_tile<OP, 13, NP>(fast, a, grid, s); break;
+    case 13: launch_tile<OP, 13, NP>(fast, a, grid, s); break;
+    case 14: launch_tile<OP, 14, NP>(fast, a, grid, s); break;
+    case 15: launch_tile<OP, 15, NP>(fast, a, grid, s); break;
+    default: launch_tile<OP, 16, NP>(fast, a, grid, s); break;
   }
 }
 

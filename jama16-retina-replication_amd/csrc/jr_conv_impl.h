@@ -430,6 +430,12 @@ static constexpr TileCfg kCfgsBf16[] = {
     {128, 128, 2, 32, 4, 0.99},  // 11: 64 KiB, 2 in flight
     {128, 96, 4, 32, 5, 0.89},   // 12: 70 KiB
     {128, 64, 2, 64, 3, 0.91},   // 13: 72 KiB, twice the MFMAs per K-tile
+    // N = 32 GEMMs (the stem: conv1 / conv2 fwd and wgrad, conv2 / conv3
+    // dgrad with N = c_in = 32), which the BN >= 64 tiles pad to twice the
+    // MFMA work: four waves stacked along M, wave tile 64 x 32 / 32 x 32
+    {256, 32, 4, 32, 3, 0.85},   // 14: 54 KiB
+    {128, 32, 4, 32, 4, 0.80},   // 15: 40 KiB
+    {256, 32, 4, 64, 3, 0.85},   // 16: 108 KiB
 };
 constexpr int kNumCfgsBf16 = sizeof(kCfgsBf16) / sizeof(kCfgsBf16[0]);
 
@@ -451,6 +457,9 @@ static constexpr TileCfg kCfgsX8P[] = {
     {128, 128, 2, 16, 5, 0.99},  // 11: 120 KiB
     {128, 96, 4, 16, 4, 0.89},   // 12: 84 KiB
     {128, 64, 2, 32, 3, 0.91},   // 13: 108 KiB
+    {256, 32, 4, 16, 3, 0.85},   // 14: 81 KiB (N = 32, as kCfgsBf16 14-16)
+    {128, 32, 4, 16, 4, 0.80},   // 15: 60 KiB
+    {256, 32, 4, 32, 2, 0.85},   // 16: 108 KiB
 };
 constexpr int kNumCfgsX8P = sizeof(kCfgsX8P) / sizeof(kCfgsX8P[0]);
 

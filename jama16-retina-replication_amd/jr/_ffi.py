@@ -50,6 +50,12 @@ class BnSeg(Structure):
                 ("beta", c_void_p), ("dbeta", c_void_p)]
 
 
+class WgradSeg(Structure):
+    """include/jr.h jr_wgrad_seg: one layer of the deferred filter-gradient reduce."""
+    _fields_ = [("slabs", c_void_p), ("dw", c_void_p)] + [(n, c_int32) for n in (
+        "m", "n", "splits", "c_in", "c_pad", "g", "block0", "blocks")]
+
+
 class PoolDesc(Structure):
     _fields_ = [(n, c_int32) for n in (
         "n", "h", "w", "c", "ho", "wo", "x_c_off", "x_c_stride", "y_c_off", "y_c_stride")]
@@ -69,6 +75,10 @@ _SIGS = {
                                    c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_bwd_filter": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_size_t, c_void_p]),
+    "jr_conv2d_wgrad_seg": (c_int, [POINTER(ConvDesc), c_int, POINTER(WgradSeg)]),
+    "jr_conv2d_bwd_filter_slabs": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_size_t,
+                                           c_void_p]),
+    "jr_wgrad_reduce": (c_int, [c_void_p, c_int32, c_int32, c_void_p]),
     "jr_conv2d_autotune": (c_int, [POINTER(ConvDesc), c_int, c_int, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_get_config": (c_int, [POINTER(ConvDesc), c_int, c_int, c_int]),

@@ -121,6 +121,8 @@ class BucketAllReduce:
         self.comm = comm
         self.payload = payload
         self.buckets = make_buckets(engine.layout, engine.nparam, bucket_bytes)
+        if hasattr(engine, "set_flush_points"):   # deferred filter-gradient slabs reduced before each bucket
+            engine.set_flush_points([lo for lo, _ in self.buckets])
         self.works = []
         self.next = 0
         dev = getattr(engine, "device", None)

@@ -65,7 +65,7 @@ class Engine:
                  optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
                  head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None,
                  autotune: bool = False, tiles: str = "pinned", fuse_siblings: bool = True, lanes: int = 2,
-                 conv_math: Optional[str] = None):
+                 conv_math: Optional[str] = None, defer_wgrad: bool = True):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if conv_math is None:            # fp32 default: x8 (fp32-accurate, on the bf16 matrix cores)
@@ -112,6 +112,12 @@ class Engine:
         self._alloc()
         self.load_params(init_params(self.g, seed))
         self._calls: Dict[int, Tuple[list, list, list]] = {}
+        self._retired: list = []        # call sets a captured graph may still reference
+        # filter gradients of split-K wgrad GEMMs: slabs kept per layer and
+        # summed by ONE jr_wgrad_reduce launch per flush point (the end of the
+        # backward, and each gradient bucket's issue point: set_flush_points)
+        self.defer_wgrad = bool(defer_wgrad)
+        self._flush_points: List[int] = []
         self._graphs: Dict[int, int] = {}
         self.bucket_hooks: List[Tuple[int, Callable]] = []
         # conv tiles: "pinned" = the committed MI355X table for this workload
@@ -278,6 +284,7 @@ class Engine:
         caches the fastest in libjr).  Runs before any data is loaded: it
         overwrites raw / gradient buffers."""
         L, B = self.lib, self.batch
+        self._drop_calls()
         ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
         s = self._s
         if self.dt == _ffi.JR_BF16 or self.x8p:
@@ -324,8 +331,23 @@ class Engine:
                 "width": self.g.width, "configs": {k: [f, wg, list(dg)] for k, (f, wg, dg) in
                                                    self.conv_configs().items()}}
 
+    def _drop_calls(self) -> None:
+        """Forget the bound call lists (tile plans or flush points changed);
+        their buffers stay alive for graphs captured from them."""
+        self._retired.extend(self._calls.values())
+        self._calls.clear()
+
+    def set_flush_points(self, points) -> None:
+        """Flat-gradient offsets at which a consumer (jr.dist.BucketAllReduce)
+        needs every gradient at offsets >= the point final: the deferred
+        filter-gradient slabs are reduced before the param_ready hook of the
+        first launch whose offset is <= the point."""
+        self._flush_points = sorted((int(p) for p in points), reverse=True)
+        self._drop_calls()
+
     def set_tile_table(self, table: dict) -> None:
         """Pin every conv launch to the configs of `table` (tile_table())."""
+        self._drop_calls()
         if (table.get("conv_math"), table.get("batch"), table.get("height"), table.get("width")) != \
                 (self.conv_math, self.batch, self.g.height, self.g.width):
             raise ValueError("tile table is for another conv math / batch / resolution")
@@ -346,6 +368,8 @@ class Engine:
     def clear_tile_table(self) -> None:
         """Back to the deterministic planner heuristic for every conv launch
         (drops autotuned or pinned configs of this engine's geometries)."""
+        if hasattr(self, "_calls"):
+            self._drop_calls()
         for u in self.cunits:
             d = self._conv_desc(u, self.batch)
             ops = [(_ffi.JR_CONV_FWD, 0)]
@@ -494,6 +518,44 @@ class Engine:
             "head_fwd", 0, [("feat",), ("p",), ("lab",)], [("head",)])
         if self.train_mode:
             D = lambda bid: self.dacts[bid].data_ptr()  # noqa: E731
+            # deferred filter gradients: per-layer slab regions of one arena
+            defer: Dict[int, Tuple[_ffi.WgradSeg, int, int]] = {}
+            if self.defer_wgrad:
+                off = 0
+                for u in self.cunits:
+                    d = self._conv_desc(u, B)
+                    keep.append(d)
+                    sg = _ffi.WgradSeg()
+                    _ffi.check("jr_conv2d_wgrad_seg", L.jr_conv2d_wgrad_seg(ctypes.byref(d), cdt, ctypes.byref(sg)))
+                    if sg.splits > 1:
+                        nb = 4 * sg.splits * sg.m * sg.n
+                        sg.dw = self.grads.data_ptr() + 4 * u.koff
+                        defer[u.first.idx] = (sg, off, nb)
+                        off += (nb + 255) // 256 * 256
+                arena = self._t(off // 4 + 64)
+                keep.append(arena)
+                for sg, o, _ in defer.values():
+                    sg.slabs = arena.data_ptr() + o
+                self.slab_bytes = off
+            pending: List[Tuple[_ffi.WgradSeg, int]] = []
+            flush_at = list(self._flush_points)
+
+            def flush():
+                """One jr_wgrad_reduce over every pending layer (lane 0)."""
+                if not pending:
+                    return
+                arr = (_ffi.WgradSeg * len(pending))()
+                blocks = 0
+                for k, (sg, _) in enumerate(pending):
+                    arr[k] = sg
+                    arr[k].block0 = blocks
+                    blocks += sg.blocks
+                table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
+                keep.append(table)
+                nbytes = sum(4 * sg.m * sg.n * (sg.splits + 1) for sg, _ in pending)
+                add(bwd, L.jr_wgrad_reduce, (table.data_ptr(), len(pending), blocks, S[0]), "wgrad_reduce", 0,
+                    [("slab", uid) for _, uid in pending], [("g", uid) for _, uid in pending], nbytes=nbytes)
+                pending.clear()
             add(bwd, L.jr_head_bwd, (self.head_mode, self.feat.data_ptr(), self._p("dense/kernel"),
                                      self.probs.data_ptr(), self.labels.data_ptr(), B, ob.c, self.units,
                                      self.dfeat.data_ptr(), self._gp("dense/kernel"), self._gp("dense/bias"), s0),
@@ -543,14 +605,26 @@ class Engine:
                         add(bwd, L.jr_split_x8p, (draw, M, u.cout, 0, u.cout, drawp, u.cout, 0, u.cout, M * u.cout, s),
                             "split_x8p", ln, [("draw", ln)], [("drawp", ln)], nbytes=10 * M * u.cout)
                         draw, dkey = drawp, ("drawp", ln)
-                    add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), cdt, AX(u.x), draw,
-                                                      self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
-                        "conv_wgrad", ln, ax_reads(u.x) + [dkey], [("g", uid), ("ws", ln)])
+                    if uid in defer:
+                        sg, _, nb = defer[uid]
+                        add(bwd, L.jr_conv2d_bwd_filter_slabs, (ctypes.byref(d), cdt, AX(u.x), draw, sg.slabs, nb, s),
+                            "conv_wgrad", ln, ax_reads(u.x) + [dkey], [("slab", uid)])
+                        pending.append((sg, uid))
+                    else:
+                        add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), cdt, AX(u.x), draw,
+                                                          self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
+                            "conv_wgrad", ln, ax_reads(u.x) + [dkey], [("g", uid), ("ws", ln)])
                     if u.x != g.input_buf:
                         add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), cdt, draw, self._wd(u), D(u.x), acc, ws, wsb,
                                                         s),
                             "conv_dgrad", ln, [dkey, wkey], d_all(u.x) + [("ws", ln)])
                         written.add(u.x)
+                    trigger = False
+                    while flush_at and flush_at[0] >= u.koff:
+                        flush_at.pop(0)
+                        trigger = True
+                    if trigger:
+                        flush()
                     bwd.append(Call("param_ready", u.koff, "hook", 0))
                 elif n.kind == "maxpool":
                     d = self._pool_desc(n, B)
@@ -567,6 +641,7 @@ class Engine:
                         "avgpool_bwd", ln, [("d", n.y.buf, n.y.c_off)], d_all(n.x),
                         nbytes=B * n.c * (n.ho * n.wo + n.h * n.w * (1 + acc)) * self.esz)
                     written.add(n.x)
+            flush()
             P, G = self.params.data_ptr(), self.grads.data_ptr()
             greads = [("g", u.first.idx) for u in self.cunits] + [("g", "dense")]
             if self.optimizer == "nesterov":
@@ -746,10 +821,4 @@ class Engine:
         try:
             self.close()
         except Exception:   # interpreter shutdown: the library may be gone
-            pass
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
             pass

@@ -201,6 +201,45 @@ def test_lanes_are_bitwise_single_stream(dtype):
         assert one.loss_value() == e.loss_value()
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_deferred_wgrad_reduce_is_bitwise(dtype):
+    """Filter gradients of split-K wgrad GEMMs left as slabs and summed by ONE
+    jr_wgrad_reduce launch (at the end of the backward, or before each
+    gradient bucket: set_flush_points) are bitwise the per-layer reduce's,
+    eagerly and as a HIP graph, over several steps."""
+    from jr.engine import Engine
+    from jr import synth
+    imgs = synth.fundus_batch(4, 4, 139)
+    y = np.array([[1.0], [0.0], [0.0], [1.0]], np.float32)
+    ref = Engine(4, 139, 139, seed=8, dtype=dtype, defer_wgrad=False)
+    dfr = Engine(4, 139, 139, seed=8, dtype=dtype)
+    pts = Engine(4, 139, 139, seed=8, dtype=dtype)
+    gr = Engine(4, 139, 139, seed=8, dtype=dtype)
+    pts.set_flush_points([pts.nparam // 2, pts.nparam // 5, pts.nparam // 20])
+    _, bwd, _, _, _ = pts._build_calls(4)
+    assert sum(c.name == "wgrad_reduce" for c in bwd) >= 2
+    _, bwd, _, _, _ = dfr._build_calls(4)
+    assert sum(c.name == "wgrad_reduce" for c in bwd) == 1 and dfr.slab_bytes > 0
+    for e in (ref, dfr, pts, gr):
+        e.set_batch(imgs, y)
+    ref.forward(); ref.backward()
+    dfr.forward(); dfr.backward()
+    assert np.array_equal(ref.grads_numpy(), dfr.grads_numpy())
+    ref.apply_update(); dfr.apply_update()
+    gr.train_step()
+    gr.capture()
+    pts.train_step()
+    for _ in range(2):
+        ref.train_step()
+        dfr.train_step()
+        pts.train_step()
+        gr.replay()
+    for e in (dfr, pts, gr):
+        e.synchronize()
+        assert np.array_equal(ref.params_numpy(), e.params_numpy())
+        assert ref.loss_value() == e.loss_value()
+
+
 def test_ensemble_auc_matches_oracle():
     """evaluate.py's ensemble (evaluate.py:214-217 + lib/evaluation.py): M
     members' sigmoid predictions over the test batches (batch statistics per

@@ -5,7 +5,8 @@ jr_conv2d_autotune's two-pass search (every tile at the planner's split, then
 other splits for the three fastest tiles) may miss.
   python tools/conv_sweep.py <dtype 0|1|2|3> <op 0|1|2> <layer> [reps]
 layers: c17x7 (17^2 192->192 1x7 same), c17x1 (17^2 768->192 1x1), c35x3 (35^2 64->96 3x3 same),
-        c8x3 (8^2 384->384 1x3 same), conv5 (73^2 80->192 3x3 valid)."""
+        c8x3 (8^2 384->384 1x3 same), conv5 (73^2 80->192 3x3 valid), conv1 (299^2 3->32 3x3/2 valid),
+        conv2 (149^2 32->32 3x3 valid), conv3 (147^2 32->64 3x3 same)."""
 import ctypes
 import os
 import sys
@@ -17,7 +18,8 @@ from jr import _ffi  # noqa: E402
 # n, h, w, cin, cout, kh, kw, stride, ph, pw
 LAYERS = {"c17x7": (64, 17, 17, 192, 192, 1, 7, 1, 0, 3), "c17x1": (64, 17, 17, 768, 192, 1, 1, 1, 0, 0),
           "c35x3": (64, 35, 35, 64, 96, 3, 3, 1, 1, 1), "c8x3": (64, 8, 8, 384, 384, 1, 3, 1, 0, 1),
-          "conv5": (64, 73, 73, 80, 192, 3, 3, 1, 0, 0)}
+          "conv5": (64, 73, 73, 80, 192, 3, 3, 1, 0, 0), "conv1": (64, 299, 299, 3, 32, 3, 3, 2, 0, 0),
+          "conv2": (64, 149, 149, 32, 32, 3, 3, 1, 0, 0), "conv3": (64, 147, 147, 32, 64, 3, 3, 1, 1, 1)}
 dt, op, layer = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
 reps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 _ffi.init(0)
