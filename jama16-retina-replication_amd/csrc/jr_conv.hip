@@ -617,11 +617,24 @@ static int chan_pad(int c, int dtype) {
   const int q = bf16_operands(dtype) ? 8 : 4;
   return (c + q - 1) / q * q;
 }
-static const TileCfg* cfg_table(int dtype) {
-  return dtype == JR_BF16 ? kCfgsBf16 : dtype == JR_F32_X8P ? kCfgsX8P : kCfgs;
-}
-static int cfg_count(int dtype) {
+// GEMM tiles of a dtype (the planner heuristic ranks these), and every
+// selectable config: for JR_BF16 the halo-tiled FWD configs follow them.
+static int std_count(int dtype) {
   return dtype == JR_BF16 ? kNumCfgsBf16 : dtype == JR_F32_X8P ? kNumCfgsX8P : kNumCfgs;
+}
+static int cfg_count(int dtype) { return std_count(dtype) + (dtype == JR_BF16 ? kNumHaloBf16 : 0); }
+static bool is_halo(int dtype, int tile) { return dtype == JR_BF16 && tile >= kNumCfgsBf16; }
+static const TileCfg& tile_cfg(int dtype, int tile) {
+  if (is_halo(dtype, tile)) return kHaloBf16[tile - kNumCfgsBf16].t;
+  return (dtype == JR_BF16 ? kCfgsBf16 : dtype == JR_F32_X8P ? kCfgsX8P : kCfgs)[tile];
+}
+// Halo rows a BM-row tile needs: output rows it spans (bound) + kh - 1.
+static int halo_rows(const jr_conv_desc* d, int bm) { return (bm + d->wo - 2) / d->wo + 1 + d->kh - 1; }
+static bool halo_ok(const jr_conv_desc* d, int op, int dtype, int tile) {
+  if (!is_halo(dtype, tile) || op != OP_FWD) return false;
+  const HaloCfg& h = kHaloBf16[tile - kNumCfgsBf16];
+  return d->kh == h.kh && d->kw == h.kw && d->stride_h == 1 && d->stride_w == 1 && d->ho == d->h &&
+         d->wo == d->w && d->c_in % 32 == 0 && halo_rows(d, h.t.bm) * (d->w + d->kw - 1) < h.slots;
 }
 
 static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
@@ -647,7 +660,7 @@ static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
 static Plan plan_with(int dtype, int cfg, int M, int N, int K) {
   Plan p{};
   p.M = M; p.N = N; p.K = K; p.cfg = cfg; p.tile = cfg_tile(cfg);
-  const TileCfg& t = cfg_table(dtype)[p.tile];
+  const TileCfg& t = tile_cfg(dtype, p.tile);
   p.mt = (int)ceil_div(M, t.bm);
   p.nt = (int)ceil_div(N, t.bn);
   p.ktiles = (int)ceil_div(K, t.bk);
@@ -668,8 +681,8 @@ static Plan plan_with(int dtype, int cfg, int M, int N, int K) {
 static int heuristic_cfg(int dtype, int M, int N, int K) {
   double best = 1e300;
   int bc = 0;
-  for (int c = 0; c < cfg_count(dtype); ++c) {
-    const TileCfg& t = cfg_table(dtype)[c];
+  for (int c = 0; c < std_count(dtype); ++c) {
+    const TileCfg& t = tile_cfg(dtype, c);
     const double tiles = (double)ceil_div(M, t.bm) * ceil_div(N, t.bn);
     double work = tiles * t.bm * t.bn / t.eff;
     // grids that cannot fill the 256 CUs and cannot be split along K lose
@@ -695,7 +708,9 @@ static Plan make_plan(int dtype, int op, int M, int N, int K, const jr_conv_desc
     auto it = g_tuned.find(tune_key(dtype, op, M, N, K, d));
     if (it != g_tuned.end()) cfg = it->second;
   }
-  if (cfg < 0) cfg = heuristic_cfg(dtype, M, N, K);
+  // a halo config (tuned, pinned or forced) only where its geometry holds
+  if (cfg < 0 || (is_halo(dtype, cfg_tile(cfg)) && !halo_ok(d, op, dtype, cfg_tile(cfg))))
+    cfg = heuristic_cfg(dtype, M, N, K);
   return plan_with(dtype, cfg, M, N, K);
 }
 
@@ -722,7 +737,7 @@ struct StatsReq {
 };
 
 static void stats_geom(int dtype, const Plan& p, int* P, int* R) {
-  const TileCfg& t = cfg_table(dtype)[p.tile];
+  const TileCfg& t = tile_cfg(dtype, p.tile);
   if (p.splits <= 1) {
     *R = t.bm / t.wgm;
     *P = p.mt * t.wgm;
@@ -849,8 +864,13 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     a.C = static_cast<float*>(out);
   }
   dim3 grid(p.mt * p.nt, 1, p.splits);
-  if (bf16_operands(dtype)) {
-    const TileCfg& t = cfg_table(dtype)[p.tile];
+  if (is_halo(dtype, p.tile)) {
+    const HaloCfg& h = kHaloBf16[p.tile - kNumCfgsBf16];
+    a.halo_wp = a.w + a.kw - 1;
+    a.halo_nr = (h.t.bm + a.wo - 2) / a.wo + 1 + a.kh - 1;
+    launch_conv_halo(p.tile - kNumCfgsBf16, a, grid, s);
+  } else if (bf16_operands(dtype)) {
+    const TileCfg& t = tile_cfg(dtype, p.tile);
     const bool fast = OP == OP_WGRAD ? a.wo >= t.bk : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
     launch_conv_bf16(OP, p.tile, fast, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
   } else if (dtype == JR_F32_X8) {
@@ -1017,6 +1037,7 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
     int best_c = heuristic_cfg(dtype, M, N, K);
     float best_t = 1e30f;
     auto time_cfg = [&](int c) -> float {
+      if (is_halo(dtype, cfg_tile(c)) && !halo_ok(d, op, dtype, cfg_tile(c))) return 1e30f;
       const Plan pc = plan_with(dtype, c, M, N, K);
       // FWD runs with the fused BN statistics: their partials must fit too
       if ((op == OP_FWD ? align256(plan_ws(pc)) + stats_ws(dtype, pc) : plan_ws(pc)) > ws_bytes) return 1e30f;

@@ -34,6 +34,8 @@ struct ConvArgs {
   int py, px, r0, c0, na, nb, ey, ex, hc, wc;
   // JR_F32_X8P: element stride between the h, m and l planes of A and of B
   long long a_ps, b_ps;
+  // halo-tiled FWD (jr_conv_halo.hip): halo rows per block and slot columns
+  int halo_nr, halo_wp;
 };
 
 // Output element offset of GEMM row m (column 0), or -1 to drop the row.
@@ -462,6 +464,29 @@ static constexpr TileCfg kCfgsX8P[] = {
     {256, 32, 4, 32, 2, 0.85},   // 16: 108 KiB
 };
 constexpr int kNumCfgsX8P = sizeof(kCfgsX8P) / sizeof(kCfgsX8P[0]);
+
+// Halo-tiled bf16 FWD configurations (jr_conv_halo.hip), bf16 tile ids
+// kNumCfgsBf16 + i: for stride-1 'same' convs of exactly this kh x kw with
+// c_in % 32 == 0 whose halo (output rows a BM tile spans + kh - 1) x (w + kw -
+// 1) fits in slots - 1 (the last slot stays zero).  t.bk = kh*kw*32 (one
+// K-tile = one 32-channel chunk of every tap), so the planner's ktiles is
+// the chunk count.  LDS per stage: slots x 64 B + kh*kw x BN x 64 B.
+struct HaloCfg {
+  int kh, kw, slots;
+  TileCfg t;
+};
+static constexpr HaloCfg kHaloBf16[] = {
+    {1, 7, 224, {128, 64, 2, 7 * 32, 2, 1.0}},   // 0: 17^2 1x7: 9 x 23 = 207 slots; 2 x 42 KiB
+    {7, 1, 256, {128, 64, 2, 7 * 32, 2, 1.0}},   // 1: 17^2 7x1: 15 x 17 = 255 slots; 2 x 44 KiB
+    {3, 3, 272, {128, 96, 4, 9 * 32, 2, 1.0}},   // 2: 35^2 3x3, N = 96: 7 x 37 = 259 slots; 2 x 71 KiB
+    {3, 3, 272, {128, 64, 2, 9 * 32, 2, 1.0}},   // 3: 3x3, N = 64 tiles (8^2: 19 x 10 = 190 slots); 2 x 53 KiB
+    {1, 3, 176, {128, 64, 2, 3 * 32, 3, 1.0}},   // 4: 8^2 1x3: 17 x 10 = 170 slots; 3 x 23 KiB
+    {3, 1, 160, {128, 64, 2, 3 * 32, 3, 1.0}},   // 5: 8^2 3x1: 19 x 8 = 152 slots; 3 x 22 KiB
+    {1, 7, 224, {128, 64, 2, 7 * 32, 3, 1.0}},   // 6: as 0, three stages (126 KiB)
+    {7, 1, 256, {128, 64, 2, 7 * 32, 3, 1.0}},   // 7: as 1, three stages (132 KiB)
+};
+constexpr int kNumHaloBf16 = sizeof(kHaloBf16) / sizeof(kHaloBf16[0]);
+void launch_conv_halo(int h, const ConvArgs& a, dim3 grid, hipStream_t s);
 
 // bf16-operand GEMM launch (jr_conv_bf16.hip): tile index into kCfgsBf16
 // (np = 1, JR_BF16) or kCfgsX8P (np = 3, JR_F32_X8P), fast = the

@@ -172,6 +172,57 @@ def test_conv_bf16_every_tile_config(case):
                 assert out["dgrad"] < TOL_BF16_OUT, (t, sp, out)
 
 
+@pytest.mark.parametrize("case", [(2, 17, 17, 128, 192, 1, 7, 1, "same"), (2, 17, 17, 160, 160, 7, 1, 1, "same"),
+                                  (2, 35, 35, 64, 96, 3, 3, 1, "same"), (2, 8, 8, 448, 384, 3, 3, 1, "same"),
+                                  (2, 8, 8, 384, 384, 1, 3, 1, "same"), (2, 8, 8, 384, 384, 3, 1, 1, "same"),
+                                  (1, 29, 31, 32, 48, 3, 3, 1, "same")])
+def test_conv_bf16_halo_configs(case):
+    """The halo-tiled forward (jr_conv_halo.hip: one halo image per 32-channel
+    chunk, every tap a shifted window of it; the last 8 bf16 config ids)
+    against the fp64 oracle, with the planner's split-K factor and forced
+    factor 2, and with the fused BN statistics.  A halo config forced on a
+    geometry it does not cover falls back to the GEMM tiles (dgrad / wgrad
+    here), and at least one halo config takes every case's forward."""
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, cin, cout, kh, kw, s, pad = case
+    nc = L.jr_conv2d_num_configs(1)
+    taken = 0
+    extra = 4 * 4 * n * h * w * 8 * cout
+    for t in range(nc - 8, nc):
+        for sp in (0, 2):
+            out = _run_all(ffi, L, case, seed=21, cfg=t | (sp << 8), extra_ws=extra)
+            assert out["fwd"] < TOL_BF16_OUT and out["wgrad"] < TOL_F32_OUT, (t, sp, out)
+            assert out["dgrad"] < TOL_BF16_OUT, (t, sp, out)
+            d, ho, wo = _desc(ffi, n, h, w, cin, cout, kh, kw, s, pad, (cin + 7) // 8 * 8)
+            taken += (L.jr_conv2d_get_config(ctypes.byref(d), 0, 1, 0) & 0xFF) == t
+    assert taken > 0, case
+    # fused BN statistics through the halo epilogue
+    rng = np.random.default_rng(5)
+    x = bf16_round(rng.standard_normal((n, h, w, cin)))
+    wt32 = (rng.standard_normal((kh, kw, cin, cout)) / np.sqrt(kh * kw * cin)).astype(np.float32)
+    d, ho, wo = _desc(ffi, n, h, w, cin, cout, kh, kw, s, pad, cin)
+    hwio, wtt = _weights(ffi, L, wt32)
+    X = dev_bf16(x)
+    wsb = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, 1)
+    ws = torch.zeros(wsb // 4 + 4, device="cuda")
+    Y = torch.zeros(n * ho * wo * cout, dtype=torch.bfloat16, device="cuda")
+    MEAN, INV = torch.zeros(cout, device="cuda"), torch.zeros(cout, device="cuda")
+    for t in range(nc - 8, nc):
+        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, 1, 0, t))
+        if (L.jr_conv2d_get_config(ctypes.byref(d), 0, 1, 0) & 0xFF) != t:
+            continue
+        ffi.check("fwd+stats", L.jr_conv2d_fwd_bn_stats(ctypes.byref(d), 1, X.data_ptr(), wtt.data_ptr(), Y.data_ptr(),
+                                                         ctypes.c_float(1e-3), MEAN.data_ptr(), INV.data_ptr(),
+                                                         ws.data_ptr(), wsb, None))
+        y = host(Y).reshape(n * ho * wo, cout).astype(np.float64)   # statistics are of y as stored
+        mu = y.mean(0)
+        inv = 1.0 / np.sqrt(y.var(0) + 1e-3)
+        assert np.max(np.abs(MEAN.cpu().numpy() - mu)) <= 1e-5 * np.abs(y).max(), t
+        assert np.max(np.abs(INV.cpu().numpy() / inv - 1)) <= 1e-5, t
+    ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, 1, 0, -1))
+
+
 def test_conv_weights_bf16_layouts():
     """jr_conv_weights_bf16 and the one-launch multi-layer form write the
     bf16 HWIO copy and the zero-padded W^T [co][kh][kw][c8] exactly."""

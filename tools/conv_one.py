@@ -1,6 +1,7 @@
 """Run one conv op repeatedly (for rocprofv3 --pmc passes and timing):
   python tools/conv_one.py <dtype 0|1|2|3> <op 0|1|2> <cfg|-1> [layer] [reps]
-layers: conv5 (73^2 80->192 3x3, B=64), m17 (17^2 768->512 1x1), m8 (8^2 448->384 3x3)."""
+layers: conv5 (73^2 80->192 3x3, B=64), m17 (17^2 768->512 1x1), m8 (8^2 448->384 3x3),
+        conv3, c17x7 (17^2 192->192 1x7 same), c35x3 (35^2 64->96 3x3 same)."""
 import ctypes
 import os
 import sys
@@ -10,15 +11,18 @@ import torch  # noqa: E402
 from jr import _ffi  # noqa: E402
 
 LAYERS = {"conv5": (64, 73, 73, 80, 192, 3, 3, 1, 0), "m17": (64, 17, 17, 768, 512, 1, 1, 1, 0),
-          "m8": (64, 8, 8, 448, 384, 3, 3, 1, 1), "conv3": (64, 147, 147, 32, 64, 3, 3, 1, 1)}
+          "m8": (64, 8, 8, 448, 384, 3, 3, 1, 1), "conv3": (64, 147, 147, 32, 64, 3, 3, 1, 1),
+          "c17x7": (64, 17, 17, 192, 192, 1, 7, 1, 0, 3), "c35x3": (64, 35, 35, 64, 96, 3, 3, 1, 1, 1)}
 dt, op, cfg = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 layer = sys.argv[4] if len(sys.argv) > 4 else "conv5"
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 20
 _ffi.init(0)
 L = _ffi.load()
-n, h, w, ci, co, kh, kw, s, p = LAYERS[layer]
-ho, wo = (h + 2 * p - kh) // s + 1, (w + 2 * p - kw) // s + 1
-d = _ffi.ConvDesc(n, h, w, ci, co, kh, kw, s, s, p, p, ho, wo, 0, ci, 0, co)
+geo = LAYERS[layer]
+n, h, w, ci, co, kh, kw, s = geo[:8]
+ph, pw = geo[8:] if len(geo) == 10 else (geo[8], geo[8])
+ho, wo = (h + 2 * ph - kh) // s + 1, (w + 2 * pw - kw) // s + 1
+d = _ffi.ConvDesc(n, h, w, ci, co, kh, kw, s, s, ph, pw, ho, wo, 0, ci, 0, co)
 pl = 3 if dt == 3 else 1
 et = torch.bfloat16 if dt in (1, 3) else torch.float32
 ot = torch.bfloat16 if dt == 1 else torch.float32

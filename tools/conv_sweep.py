@@ -19,7 +19,9 @@ from jr import _ffi  # noqa: E402
 LAYERS = {"c17x7": (64, 17, 17, 192, 192, 1, 7, 1, 0, 3), "c17x1": (64, 17, 17, 768, 192, 1, 1, 1, 0, 0),
           "c35x3": (64, 35, 35, 64, 96, 3, 3, 1, 1, 1), "c8x3": (64, 8, 8, 384, 384, 1, 3, 1, 0, 1),
           "conv5": (64, 73, 73, 80, 192, 3, 3, 1, 0, 0), "conv1": (64, 299, 299, 3, 32, 3, 3, 2, 0, 0),
-          "conv2": (64, 149, 149, 32, 32, 3, 3, 1, 0, 0), "conv3": (64, 147, 147, 32, 64, 3, 3, 1, 1, 1)}
+          "conv2": (64, 149, 149, 32, 32, 3, 3, 1, 0, 0), "conv3": (64, 147, 147, 32, 64, 3, 3, 1, 1, 1),
+          "c17x7v": (64, 17, 17, 192, 192, 7, 1, 1, 3, 0), "c8x3v": (64, 8, 8, 384, 384, 3, 1, 1, 1, 0),
+          "c8x33": (64, 8, 8, 448, 384, 3, 3, 1, 1, 1), "c35x33": (64, 35, 35, 96, 96, 3, 3, 1, 1, 1)}
 dt, op, layer = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
 reps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 _ffi.init(0)
@@ -60,8 +62,8 @@ for tile in range(L.jr_conv2d_num_configs(dt)):
     for sp in (1, 2, 3, 4, 6, 8, 12, 16, 32, 64):
         cfg = tile | (sp << 8)
         ok = all(L.jr_conv2d_set_config(ctypes.byref(d), op, dt, p, cfg) == 0 for p in range(nph))
-        if not ok or run() != 0:
-            continue
+        if not ok or (L.jr_conv2d_get_config(ctypes.byref(d), op, dt, 0) & 255) != tile or run() != 0:
+            continue        # (a halo config this geometry does not take falls back: skipped)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

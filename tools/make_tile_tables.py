@@ -7,7 +7,9 @@ between neighbours).  Regenerate whenever a tile table in
 csrc/jr_conv_impl.h changes (tests/test_tile_tables.py checks every id is in
 range of jr_conv2d_num_configs).
 
-  python tools/make_tile_tables.py [out.json]     (GPU box)"""
+  python tools/make_tile_tables.py [out.json] [conv_math ...]     (GPU box)
+With conv maths listed (e.g. bf16), only those workloads are re-tuned and the
+other tables of the existing file are kept."""
 import collections
 import json
 import os
@@ -40,10 +42,16 @@ def tune(dtype, math, B, res, train):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "jama16-retina-replication_amd", "jr",
-                                                             "tiles_mi355x.json")
+    default = os.path.join(ROOT, "jama16-retina-replication_amd", "jr", "tiles_mi355x.json")
+    out = sys.argv[1] if len(sys.argv) > 1 else default
+    only = set(sys.argv[2:])
     tables = []
+    if only:
+        with open(default) as f:
+            tables = [t for t in json.load(f)["tables"] if t["conv_math"] not in only]
     for w in WORKLOADS:
+        if only and w[1] not in only:
+            continue
         t0 = time.time()
         runs = []
         for r in range(REPS):
