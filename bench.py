@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-defer-wgrad", action="store_true",
                     help="reduce each split-K filter gradient right after its GEMM (A/B of jr_wgrad_reduce)")
+    ap.add_argument("--bn-fuse", action="store_true",
+                    help="BN-backward reduce in the last-writer dgrad epilogue (Engine(bn_fuse=True); A/B)")
     return ap.parse_args()
 
 
@@ -259,7 +261,7 @@ def main():
     B, res = args.batch or (64 if train else 32), args.res
     math = args.conv_math if args.dtype == "f32" else "bf16"
     eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0, lanes=args.lanes, train=train,
-                 conv_math=math, tiles=args.tiles, defer_wgrad=not args.no_defer_wgrad)
+                 conv_math=math, tiles=args.tiles, defer_wgrad=not args.no_defer_wgrad, bn_fuse=args.bn_fuse)
     imgs = synth.fundus_batch(rank * B, B, res)
     labels = synth.labels(rank * B, B)
     eng.set_batch(imgs, labels)

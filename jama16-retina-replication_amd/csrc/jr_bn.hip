@@ -311,6 +311,50 @@ __global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ 
   }
 }
 
+// The MODE 1 combine for many partials (jr_bn_relu_bwd_parts: one per row
+// group of the data-gradient GEMM, ~22k for the stem layers): one block per
+// channel, thread t sums slots t, t + 256, ... with 8 loads in flight, then a
+// fixed tree -- deterministic.
+__global__ void __launch_bounds__(256) k_bn_finalize_big(const double* __restrict__ part, int P, int c, int64_t m,
+                                                         float* k1, float* k2, BnSegs sg) {
+  __shared__ double red[2][256];
+  const int k = blockIdx.x, t = threadIdx.x;
+  const double* p0 = part + (int64_t)k * P;
+  const double* p1 = part + (int64_t)(c + k) * P;
+  double a = 0.0, b = 0.0;
+  for (int i0 = 0; i0 < P; i0 += 256 * 8) {
+    double va[8], vb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {   // clamped, unconditional loads (kept in flight together)
+      const int i = min(i0 + u * 256 + t, P - 1);
+      va[u] = p0[i];
+      vb[u] = p1[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool ok = i0 + u * 256 + t < P;
+      a += ok ? va[u] : 0.0;
+      b += ok ? vb[u] : 0.0;
+    }
+  }
+  red[0][t] = a;
+  red[1][t] = b;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (t < h) {
+      red[0][t] += red[0][t + h];
+      red[1][t] += red[1][t + h];
+    }
+    __syncthreads();
+  }
+  if (t != 0) return;
+  const double inv_m = 1.0 / (double)m;
+  k1[k] = (float)(red[0][0] * inv_m);
+  k2[k] = (float)(red[1][0] * inv_m);
+  const int sgi = seg_of(sg, k);
+  sg.dbeta[sgi][k - sg.c0[sgi]] = (float)red[0][0];
+}
+
 // Elementwise passes: block b covers rows [b*rpp*U, (b+1)*rpp*U), thread
 // (q, rr) rows rr, rr+rpp, ...; per-channel constants loaded once.
 template <typename T>
@@ -475,6 +519,20 @@ JR_API int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x
   return check_launch("bn_relu_apply");
 }
 
+// The apply pass of the backward (k1, k2 from a finalize).
+static int bn_bwd_apply_launch(int dtype, const BnSegs& sg, const void* x, int32_t x_c_stride, int64_t m, int32_t c,
+                               const float* mean, const float* invstd, const float* k1, const float* k2, void* dx,
+                               hipStream_t s) {
+  const int grid = apply_grid(m, c, vec_width(dtype));
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_bn_relu_bwd_apply<float>, dim3(grid), dim3(256), 0, s, sg, (const float*)x, x_c_stride, m,
+                       c, mean, invstd, k1, k2, (float*)dx);
+  else
+    hipLaunchKernelGGL(k_bn_relu_bwd_apply<uint16_t>, dim3(grid), dim3(256), 0, s, sg, (const uint16_t*)x,
+                       x_c_stride, m, c, mean, invstd, k1, k2, (uint16_t*)dx);
+  return check_launch("bn_bwd apply");
+}
+
 // The three backward launches over segments (validated by the callers).
 static int bn_bwd_launch(int dtype, const BnSegs& sg, const void* x, int32_t x_c_stride, int64_t m, int32_t c,
                          const float* mean, const float* invstd, void* dx, void* ws, size_t ws_bytes,
@@ -497,14 +555,7 @@ static int bn_bwd_launch(int dtype, const BnSegs& sg, const void* x, int32_t x_c
                      k1, k2, sg);
   rc = check_launch("bn_bwd finalize");
   if (rc) return rc;
-  const int grid = apply_grid(m, c, vw);
-  if (dtype == JR_F32)
-    hipLaunchKernelGGL(k_bn_relu_bwd_apply<float>, dim3(grid), dim3(256), 0, s, sg, (const float*)x, x_c_stride, m,
-                       c, mean, invstd, k1, k2, (float*)dx);
-  else
-    hipLaunchKernelGGL(k_bn_relu_bwd_apply<uint16_t>, dim3(grid), dim3(256), 0, s, sg, (const uint16_t*)x,
-                       x_c_stride, m, c, mean, invstd, k1, k2, (uint16_t*)dx);
-  return check_launch("bn_bwd apply");
+  return bn_bwd_apply_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, k1, k2, dx, s);
 }
 
 JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t dy_c_stride, const void* x,
@@ -515,16 +566,17 @@ JR_API int jr_bn_relu_bwd(int dtype, const void* dy, int32_t dy_c_off, int32_t d
   return jr_bn_relu_bwd_multi(dtype, 1, &seg, x, x_c_off, x_c_stride, m, c, mean, invstd, dx, ws, ws_bytes, stream);
 }
 
-JR_API int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
-                                int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd,
-                                void* dx, void* ws, size_t ws_bytes, void* stream) {
+// Validates the segments and slices of a backward launch set; on success
+// fills sg and moves x / dx to the slice's first channel.
+static int bwd_setup(int dtype, int nseg, const jr_bn_seg* segs, const void*& x, int32_t x_c_off, int32_t x_c_stride,
+                     int64_t m, int32_t c, const float* mean, const float* invstd, void*& dx, BnSegs& sg) {
   int rc = check_common(dtype, m, c);
   if (rc) return rc;
   if (!segs || nseg < 1 || nseg > kMaxSegs) return fail(JR_ERR_INVALID, "bn_relu_bwd: 1..4 segments");
   if (!x || !mean || !invstd || !dx) return fail(JR_ERR_INVALID, "bn_relu_bwd: null pointer");
   if (!check_slice(dtype, x_c_off, x_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_bwd: bad x / dx slice");
   const size_t esz = dtype == JR_BF16 ? 2 : 4;
-  BnSegs sg{};
+  sg = BnSegs{};
   sg.n = nseg;
   int c0 = 0;
   for (int i = 0; i < nseg; ++i) {
@@ -545,5 +597,38 @@ JR_API int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, cons
   sg.c0[nseg] = c;
   x = static_cast<const char*>(x) + (size_t)x_c_off * esz;
   dx = static_cast<char*>(dx) + (size_t)x_c_off * esz;
+  return JR_OK;
+}
+
+JR_API int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
+                                int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd,
+                                void* dx, void* ws, size_t ws_bytes, void* stream) {
+  BnSegs sg;
+  const int rc = bwd_setup(dtype, nseg, segs, x, x_c_off, x_c_stride, m, c, mean, invstd, dx, sg);
+  if (rc) return rc;
   return bn_bwd_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, dx, ws, ws_bytes, as_stream(stream));
 }
+
+JR_API int jr_bn_relu_bwd_parts(int dtype, int nseg, const jr_bn_seg* segs, const double* part, int32_t P,
+                                const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,
+                                const float* mean, const float* invstd, void* dx, void* ws, size_t ws_bytes,
+                                void* stream) {
+  BnSegs sg;
+  int rc = bwd_setup(dtype, nseg, segs, x, x_c_off, x_c_stride, m, c, mean, invstd, dx, sg);
+  if (rc) return rc;
+  if (!part || P < 1) return fail(JR_ERR_INVALID, "bn_relu_bwd_parts: no partials");
+  if (!ws || ws_bytes < 2 * (size_t)c * sizeof(float)) return fail(JR_ERR_WORKSPACE, "bn_relu_bwd_parts: workspace too small");
+  float* k1 = static_cast<float*>(ws);
+  float* k2 = k1 + c;
+  hipStream_t s = as_stream(stream);
+  // one wave per channel while the partials are few (k_bn_finalize's
+  // 4 loads in flight per lane), one block per channel beyond
+  if (P <= 2048)
+    hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, P, c, m, 0.f, k1, k2, sg);
+  else
+    hipLaunchKernelGGL(k_bn_finalize_big, dim3(c), dim3(256), 0, s, part, P, c, m, k1, k2, sg);
+  rc = check_launch("bn_bwd_parts finalize");
+  if (rc) return rc;
+  return bn_bwd_apply_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, k1, k2, dx, s);
+}
+
