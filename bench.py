@@ -67,8 +67,6 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-defer-wgrad", action="store_true",
                     help="reduce each split-K filter gradient right after its GEMM (A/B of jr_wgrad_reduce)")
-    ap.add_argument("--bn-fuse", action="store_true",
-                    help="BN-backward reduce in the last-writer dgrad epilogue (Engine(bn_fuse=True); A/B)")
     return ap.parse_args()
 
 
@@ -165,7 +163,7 @@ def pmc_traffic(dtype: str, B: int, res: int, math: str = "x8") -> dict:
     if (B, res) != (64, 299):
         return {}
     tag = {"f32": "f32mfma", "x8p": "f32x8p"}.get(math, "f32") if dtype == "f32" else dtype
-    for rnd in ("r02", "r01"):      # the newest committed summary of this workload
+    for rnd in ("r02c", "r02", "r01"):      # the newest committed summary of this workload
         p = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{tag}.json")
         if os.path.exists(p):
             break
@@ -261,7 +259,7 @@ def main():
     B, res = args.batch or (64 if train else 32), args.res
     math = args.conv_math if args.dtype == "f32" else "bf16"
     eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0, lanes=args.lanes, train=train,
-                 conv_math=math, tiles=args.tiles, defer_wgrad=not args.no_defer_wgrad, bn_fuse=args.bn_fuse)
+                 conv_math=math, tiles=args.tiles, defer_wgrad=not args.no_defer_wgrad)
     imgs = synth.fundus_batch(rank * B, B, res)
     labels = synth.labels(rank * B, B)
     eng.set_batch(imgs, labels)

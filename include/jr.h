@@ -123,32 +123,6 @@ int jr_conv2d_fwd_bn_stats(const jr_conv_desc* d, int dtype, const void* x, cons
 /* dx[.., x_c_off + ci] (+)= sum dy * w ; accumulate != 0 adds into dx */
 int jr_conv2d_bwd_data(const jr_conv_desc* d, int dtype, const void* dy, const void* w, void* dx,
                        int accumulate, void* ws, size_t ws_bytes, void* stream);
-/* jr_conv2d_bwd_data as the LAST writer of dx, fused with the reduce pass of
- * the BatchNormalization backward of the conv2d_bn layers whose ReLU
- * outputs are channel slices of x (replaces, for those layers, the
- * FusedBatchNormGrad / ReluGrad reduction of the Keras conv2d_bn blocks that
- * train.py:150-153's .minimize differentiates).  Slice i
- * covers dx channels [c_lo, c_hi); its layer's raw (pre-BN) conv output is
- * raw[pixel][raw_c_stride] from channel raw_c_off (same pixel grid as dx),
- * with that layer's mean / invstd / beta ([c_hi - c_lo] each).  The epilogue
- * writes, per group of rows of every phase GEMM, sum dy' and sum dy' * xhat
- * (dy' = final dx * (xhat + beta > 0), xhat = (raw - mean) * invstd) as fp64
- * into part[2][set_c][P] at channels set_off + (c - c_lo): `part` belongs to
- * the BN launch set (set_c channels) that jr_bn_relu_bwd_parts finishes.
- * P = jr_conv2d_bwd_data_bnp_slots (JR_ERR_UNSUPPORTED when the planned GEMM
- * splits K; query after the tile configuration is final).  1 <= nseg <= 6,
- * slices disjoint, c_lo a multiple of 32, c_hi a multiple of 32 or c_in. */
-typedef struct jr_bnp_seg {
-  const void* raw;
-  const float* mean;
-  const float* invstd;
-  const float* beta;
-  double* part;
-  int32_t c_lo, c_hi, raw_c_off, raw_c_stride, set_c, set_off;
-} jr_bnp_seg;
-int jr_conv2d_bwd_data_bnp_slots(const jr_conv_desc* d, int dtype, int32_t* P);
-int jr_conv2d_bwd_data_bnp(const jr_conv_desc* d, int dtype, const void* dy, const void* w, void* dx, int accumulate,
-                           int nseg, const jr_bnp_seg* segs, void* ws, size_t ws_bytes, void* stream);
 /* dw[kh][kw][ci][co] = sum x * dy  (fp32 output for both dtypes) */
 int jr_conv2d_bwd_filter(const jr_conv_desc* d, int dtype, const void* x, const void* dy, float* dw,
                          void* ws, size_t ws_bytes, void* stream);
@@ -220,14 +194,6 @@ typedef struct jr_bn_seg {
 int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
                          int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd, void* dx,
                          void* ws, size_t ws_bytes, void* stream);
-/* jr_bn_relu_bwd_multi when the reduce pass already ran in the epilogue of
- * the data-gradient GEMM(s) that wrote dy (jr_conv2d_bwd_data_bnp): part
- * holds [2][c][P] fp64 partial sums over all m rows; only the fixed-order
- * combine (k1 = sum dy'/m, k2 = sum dy'xhat/m, dbeta = sum dy') and the
- * apply pass run.  ws: >= 8 * c bytes. */
-int jr_bn_relu_bwd_parts(int dtype, int nseg, const jr_bn_seg* segs, const double* part, int32_t P, const void* x,
-                         int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c, const float* mean,
-                         const float* invstd, void* dx, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- pooling (Keras MaxPooling2D((3,3),(2,2)) / AveragePooling2D((3,3),
  *      (1,1),'same') inside InceptionV3, train.py:129-130) ------------ */

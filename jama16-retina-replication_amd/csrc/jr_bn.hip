@@ -311,50 +311,6 @@ __global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ 
   }
 }
 
-// The MODE 1 combine for many partials (jr_bn_relu_bwd_parts: one per row
-// group of the data-gradient GEMM, ~22k for the stem layers): one block per
-// channel, thread t sums slots t, t + 256, ... with 8 loads in flight, then a
-// fixed tree -- deterministic.
-__global__ void __launch_bounds__(256) k_bn_finalize_big(const double* __restrict__ part, int P, int c, int64_t m,
-                                                         float* k1, float* k2, BnSegs sg) {
-  __shared__ double red[2][256];
-  const int k = blockIdx.x, t = threadIdx.x;
-  const double* p0 = part + (int64_t)k * P;
-  const double* p1 = part + (int64_t)(c + k) * P;
-  double a = 0.0, b = 0.0;
-  for (int i0 = 0; i0 < P; i0 += 256 * 8) {
-    double va[8], vb[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {   // clamped, unconditional loads (kept in flight together)
-      const int i = min(i0 + u * 256 + t, P - 1);
-      va[u] = p0[i];
-      vb[u] = p1[i];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const bool ok = i0 + u * 256 + t < P;
-      a += ok ? va[u] : 0.0;
-      b += ok ? vb[u] : 0.0;
-    }
-  }
-  red[0][t] = a;
-  red[1][t] = b;
-  __syncthreads();
-  for (int h = 128; h > 0; h >>= 1) {
-    if (t < h) {
-      red[0][t] += red[0][t + h];
-      red[1][t] += red[1][t + h];
-    }
-    __syncthreads();
-  }
-  if (t != 0) return;
-  const double inv_m = 1.0 / (double)m;
-  k1[k] = (float)(red[0][0] * inv_m);
-  k2[k] = (float)(red[1][0] * inv_m);
-  const int sgi = seg_of(sg, k);
-  sg.dbeta[sgi][k - sg.c0[sgi]] = (float)red[0][0];
-}
-
 // Elementwise passes: block b covers rows [b*rpp*U, (b+1)*rpp*U), thread
 // (q, rr) rows rr, rr+rpp, ...; per-channel constants loaded once.
 template <typename T>
@@ -608,27 +564,3 @@ JR_API int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, cons
   if (rc) return rc;
   return bn_bwd_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, dx, ws, ws_bytes, as_stream(stream));
 }
-
-JR_API int jr_bn_relu_bwd_parts(int dtype, int nseg, const jr_bn_seg* segs, const double* part, int32_t P,
-                                const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,
-                                const float* mean, const float* invstd, void* dx, void* ws, size_t ws_bytes,
-                                void* stream) {
-  BnSegs sg;
-  int rc = bwd_setup(dtype, nseg, segs, x, x_c_off, x_c_stride, m, c, mean, invstd, dx, sg);
-  if (rc) return rc;
-  if (!part || P < 1) return fail(JR_ERR_INVALID, "bn_relu_bwd_parts: no partials");
-  if (!ws || ws_bytes < 2 * (size_t)c * sizeof(float)) return fail(JR_ERR_WORKSPACE, "bn_relu_bwd_parts: workspace too small");
-  float* k1 = static_cast<float*>(ws);
-  float* k2 = k1 + c;
-  hipStream_t s = as_stream(stream);
-  // one wave per channel while the partials are few (k_bn_finalize's
-  // 4 loads in flight per lane), one block per channel beyond
-  if (P <= 2048)
-    hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, P, c, m, 0.f, k1, k2, sg);
-  else
-    hipLaunchKernelGGL(k_bn_finalize_big, dim3(c), dim3(256), 0, s, part, P, c, m, k1, k2, sg);
-  rc = check_launch("bn_bwd_parts finalize");
-  if (rc) return rc;
-  return bn_bwd_apply_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, k1, k2, dx, s);
-}
-

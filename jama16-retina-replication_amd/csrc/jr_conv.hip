@@ -910,18 +910,6 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
   if (p.splits <= 1 || defer) return rc;
   const long long total = (long long)p.M * p.N / 4;   // float4 columns
   const int G = reduce_lanes(p);                       // z-lanes per column
-  if (OP == OP_DGRAD && a.bnp_n > 0) {   // the last writer of dx, with the BN-backward partials
-    int R, Pp;
-    reduce_rows(p.M, p.N, &R, &Pp);
-    const dim3 rg(Pp, (int)ceil_div(p.N, 1024));
-    if (dtype == JR_BF16)
-      hipLaunchKernelGGL(k_splitk_reduce_bnp<uint16_t>, rg, dim3(256), 0, s, (const float*)ws, p.splits, G, a,
-                         static_cast<uint16_t*>(out), R);
-    else
-      hipLaunchKernelGGL(k_splitk_reduce_bnp<float>, rg, dim3(256), 0, s, (const float*)ws, p.splits, G, a,
-                         static_cast<float*>(out), R);
-    return check_launch("conv split-k reduce + BN partials");
-  }
   const long long cols = 256 / G;
   const int blocks = (int)std::min<long long>(ceil_div(total, cols), 8192);
   if (dtype == JR_BF16 && OP != OP_WGRAD)   // bf16 activations / activation grads; dW stays fp32
@@ -983,37 +971,10 @@ static Plan dgrad_phase_plan(const jr_conv_desc* d, int dtype, const Phase& p, i
   return plan_for(d, OP_DGRAD, dtype, &p, force_cfg);
 }
 
-// BN-backward partial slots of a DGRAD that computes them: per phase GEMM one
-// per group of 32 rows (the epilogue), or one per row block of the split-K
-// reduce (k_splitk_reduce_bnp) when the plan splits K; phases in order
-// (slot0[i] = first slot of phase i).
-static int bnp_slots(const jr_conv_desc* d, int dtype, int* P, int* slot0) {
-  Phase ph[64];
-  int nph = 0;
-  dgrad_phases(d, ph, &nph);
-  int tot = 0;
-  for (int i = 0; i < nph; ++i) {
-    bool ok;
-    const Plan pl = dgrad_phase_plan(d, dtype, ph[i], -1, &ok);
-    if (slot0) slot0[i] = tot;
-    if (!ok) continue;
-    if (pl.splits > 1) {   // partials per row block of the split-K reduce
-      int R, Pp;
-      reduce_rows(pl.M, pl.N, &R, &Pp);
-      tot += Pp;
-    } else {               // per 32-row group of the GEMM epilogue
-      tot += pl.mt * (tile_cfg(dtype, pl.tile).bm / 32);
-    }
-  }
-  *P = tot;
-  return JR_OK;
-}
-
 // Runs the op; force_cfg >= 0 overrides the plan (autotuning).
 static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, const void* B, void* C,
                     int accumulate, void* ws, size_t ws_bytes, void* stream, int force_cfg = -1,
-                    int only_phase = -1, const StatsReq* st = nullptr, int nbnp = 0,
-                    const jr_bnp_seg* bnp = nullptr) {
+                    int only_phase = -1, const StatsReq* st = nullptr) {
   int rc = validate(d, op, dtype);
   if (rc) return rc;
   if (!A || !B || !C) return fail(JR_ERR_INVALID, "conv: null tensor pointer");
@@ -1047,31 +1008,6 @@ static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, con
   int nph = 0;
   dgrad_phases(d, ph, &nph);
   a.c_off = d->x_c_off; a.c_stride = d->x_c_stride;
-  int slot0[64];
-  if (nbnp > 0) {   // BN-backward partials in the epilogue (jr_conv2d_bwd_data_bnp)
-    if (force_cfg >= 0 || only_phase >= 0) return fail(JR_ERR_INVALID, "conv bwd_data_bnp: no forced configs");
-    rc = bnp_slots(d, dtype, &a.bnp_P, slot0);
-    if (rc) return rc;
-    a.bnp_n = nbnp;
-    for (int k = 0; k < nbnp; ++k) {
-      const jr_bnp_seg& e = bnp[k];
-      if (!e.raw || !e.mean || !e.invstd || !e.beta || !e.part)
-        return fail(JR_ERR_INVALID, "conv bwd_data_bnp: null pointer in a slice");
-      // slices start on 32-channel boundaries (the epilogue resolves one slice
-      // per 32-column block) and end on one or at c_in
-      if (e.c_lo < 0 || e.c_hi <= e.c_lo || e.c_hi > d->c_in || e.c_lo % 32 || (e.c_hi % 32 && e.c_hi != d->c_in) ||
-          e.raw_c_off < 0 || e.raw_c_off + (e.c_hi - e.c_lo) > e.raw_c_stride || e.set_off < 0 ||
-          e.set_off + (e.c_hi - e.c_lo) > e.set_c ||
-          (long long)d->n * d->h * d->w * e.raw_c_stride >= (1LL << 31))
-        return fail(JR_ERR_INVALID, "conv bwd_data_bnp: bad slice geometry");
-      for (int j = 0; j < k; ++j)
-        if (e.c_lo < bnp[j].c_hi && bnp[j].c_lo < e.c_hi) return fail(JR_ERR_INVALID, "conv bwd_data_bnp: slices overlap");
-      BnpArg& b = a.bnp[k];
-      b.raw = e.raw; b.mean = e.mean; b.invstd = e.invstd; b.beta = e.beta; b.part = e.part;
-      b.c_lo = e.c_lo; b.c_hi = e.c_hi; b.raw_off = e.raw_c_off; b.raw_stride = e.raw_c_stride;
-      b.set_c = e.set_c; b.set_off = e.set_off;
-    }
-  }
   for (int i = 0; i < nph; ++i) {
     if (only_phase >= 0 && i != only_phase) continue;
     const Phase& p = ph[i];
@@ -1080,10 +1016,8 @@ static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, con
     if (!ok) continue;
     a.py = p.py; a.px = p.px; a.r0 = p.r0; a.c0 = p.c0; a.na = p.na; a.nb = p.nb;
     a.ey = p.ey; a.ex = p.ex; a.hc = p.hc; a.wc = p.wc;
-    a.bnp_p0 = nbnp > 0 ? slot0[i] : 0;
-    // no tap reaches this phase: a K = 0 GEMM stores zeros (or leaves dx --
-    // unless it must still write its rows' BN partials)
-    if ((p.na == 0 || p.nb == 0) && accumulate && nbnp == 0) continue;
+    // no tap reaches this phase: a K = 0 GEMM stores zeros (or leaves dx)
+    if ((p.na == 0 || p.nb == 0) && accumulate) continue;
     rc = run_gemm<OP_DGRAD>(dtype, a, pl, out, ws, ws_bytes, s);
     if (rc) return rc;
   }
@@ -1343,24 +1277,6 @@ JR_API int jr_conv2d_fwd(const jr_conv_desc* d, int dtype, const void* x, const 
 JR_API int jr_conv2d_bwd_data(const jr_conv_desc* d, int dtype, const void* dy, const void* w, void* dx,
                               int accumulate, void* ws, size_t ws_bytes, void* stream) {
   return run_conv(d, OP_DGRAD, dtype, dy, w, dx, accumulate, ws, ws_bytes, stream);
-}
-
-JR_API int jr_conv2d_bwd_data_bnp_slots(const jr_conv_desc* d, int dtype, int32_t* P) {
-  int rc = validate(d, OP_DGRAD, dtype);
-  if (rc) return rc;
-  if (!P) return fail(JR_ERR_INVALID, "conv bwd_data_bnp_slots: null output");
-  int p = 0;
-  rc = bnp_slots(d, dtype, &p, nullptr);
-  if (rc) return rc;
-  *P = p;
-  return JR_OK;
-}
-
-JR_API int jr_conv2d_bwd_data_bnp(const jr_conv_desc* d, int dtype, const void* dy, const void* w, void* dx,
-                                  int accumulate, int nseg, const jr_bnp_seg* segs, void* ws, size_t ws_bytes,
-                                  void* stream) {
-  if (!segs || nseg < 1 || nseg > kMaxBnp) return fail(JR_ERR_INVALID, "conv bwd_data_bnp: 1..6 slices");
-  return run_conv(d, OP_DGRAD, dtype, dy, w, dx, accumulate, ws, ws_bytes, stream, -1, -1, nullptr, nseg, segs);
 }
 
 JR_API int jr_conv2d_bwd_filter(const jr_conv_desc* d, int dtype, const void* x, const void* dy,

@@ -16,22 +16,6 @@ enum { OP_FWD = 0, OP_DGRAD = 1, OP_WGRAD = 2 };
 // 64 B of zeros in global memory: the DMA source of out-of-bounds taps.
 static __device__ __attribute__((aligned(64))) float g_zero_page[16];
 
-// One channel slice of dx whose BatchNormalization-backward partial sums the
-// DGRAD epilogue produces (jr_conv2d_bwd_data_bnp; the device copy of
-// jr_bnp_seg): dx channels [c_lo, c_hi) are the ReLU outputs of a conv2d_bn
-// layer whose raw (pre-BN) conv output is raw[pixel][raw_stride] at channel
-// raw_off, with that layer's mean / invstd / beta; the sums land in the BN
-// launch set's partials part[2][set_c][P] at channels set_off + (c - c_lo).
-struct BnpArg {
-  const void* raw;
-  const float* mean;
-  const float* invstd;
-  const float* beta;
-  double* part;
-  int c_lo, c_hi, raw_off, raw_stride, set_c, set_off;
-};
-constexpr int kMaxBnp = 6;
-
 struct ConvArgs {
   const float* A;
   const float* B;
@@ -54,10 +38,6 @@ struct ConvArgs {
   long long a_ps, b_ps;
   // halo-tiled FWD (jr_conv_halo.hip): halo rows per block and slot columns
   int halo_nr, halo_wp;
-  // DGRAD as the last writer of dx: BN-backward partials of bnp_n slices,
-  // one per 32-row group (or split-K reduce row block) at slot bnp_p0 + group
-  int bnp_n, bnp_p0, bnp_P;
-  BnpArg bnp[kMaxBnp];
 };
 
 // Input pixel (over all images) of DGRAD row m of the phase.
@@ -183,157 +163,84 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& g, f32x16 (&acc)[T
     }
   }
   float* C = split ? g.C + (long long)blockIdx.z * g.slab_elems : g.C;
-  // DGRAD as the last writer of dx (g.bnp_n > 0, no split-K): per column of
-  // each 32-row group, the BatchNormalization-backward partial sums of the
-  // FINAL dx values (after the accumulate, bf16-rounded as stored):
-  // sum dy' and sum dy' * xhat, dy' = dy * (xhat + beta > 0), xhat =
-  // (raw - mean) * invstd with jr_bn.hip's rounding -- what k_bn_reduce<1>
-  // computes, so jr_bn_relu_bwd_parts skips that pass.  The raw conv output
-  // of the group's rows is loaded FIRST, in the accumulator layout (lane =
-  // column, 16 rows; one coalesced row segment per load, wave-uniform slice
-  // base + 32-bit offsets: slices start on 32-channel boundaries, host-
-  // checked), so those loads are in flight under the stage and store work;
-  // the store loop puts the final values back into the stage, and a column
-  // pass sums them in fp32 (a fixed xor-32 step joins the two row halves):
-  // one partial per (32-row group, channel), slot bnp_p0 + group.
-  const bool bnp = OP == OP_DGRAD && g.bnp_n > 0 && !split;
-  typedef typename std::conditional<BF16K, uint16_t, float>::type RT;
-  int sj[TN];
-  float pmu[TN], pis[TN], pbe[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    pmu[j] = pis[j] = pbe[j] = 0.f;
-    sj[j] = -1;
-    if (!bnp) continue;
-    const int nb = nw0 + j * 32;   // wave-uniform
-#pragma unroll
-    for (int q = 0; q < kMaxBnp; ++q)
-      if (q < g.bnp_n && nb >= g.bnp[q].c_lo && nb < g.bnp[q].c_hi) sj[j] = q;
-    const int n = nb + l31;
-#pragma unroll
-    for (int q = 0; q < kMaxBnp; ++q) {
-      const BnpArg& sg = g.bnp[q];
-      if (q == sj[j] && n < sg.c_hi) {
-        const int k = n - sg.c_lo;
-        pmu[j] = sg.mean[k];
-        pis[j] = sg.invstd[k];
-        pbe[j] = sg.beta[k];
-      }
-    }
-  }
-  const bool s1p = g.sh == 1 && g.sw == 1;   // stride-1 DGRAD: row m is pixel m
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    RT xr[TN][16];
-    if (bnp) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if (sj[j] < 0) continue;            // wave-uniform
-        const RT* base = nullptr;
-        int rs = 0, k = 0;
-#pragma unroll
-        for (int q = 0; q < kMaxBnp; ++q)
-          if (q == sj[j]) {
-            base = static_cast<const RT*>(g.bnp[q].raw) + g.bnp[q].raw_off;
-            rs = g.bnp[q].raw_stride;
-            k = nw0 + j * 32 + l31 - g.bnp[q].c_lo;
-            k = nw0 + j * 32 + l31 < g.bnp[q].c_hi ? k : 0;
-          }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {      // rows past M load the last row (added as zero)
-          const int m = min(mw0 + i * 32 + row_of(r), g.M - 1);
-          const int pix = s1p ? m : (int)dgrad_pix(g, m);
-          xr[j][r] = base[pix * rs + k];
-        }
-      }
-    }
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) stage[row_of(r) * S + j * 32 + l31] = acc[i][j][r];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // the group's row vectors leave in batches of CH: all stage reads and
+    // (accumulate) all old-dx loads of a batch are issued before any use --
+    // unconditional loads from clamped addresses, so one memory round trip
+    // per batch instead of one per row vector (a per-vector `continue`
+    // around the load made hipcc wait for each load in turn)
+    constexpr int CH = NIT % 4 == 0 ? 4 : NIT % 3 == 0 ? 3 : NIT % 2 == 0 ? 2 : 1;
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int e = it * 64 + lane;
-      const int row = e / LPR, c8 = (e - row * LPR) * 8;
-      const float4 v0 = *reinterpret_cast<const float4*>(stage + row * S + c8);
-      const float4 v1 = *reinterpret_cast<const float4*>(stage + row * S + c8 + 4);
-      const int m = mw0 + i * 32 + row, n = nw0 + c8;
-      if (m >= g.M || n >= g.N) continue;
-      const long long base = split ? (long long)m * g.N : out_row<OP>(g, m);
-      if (base < 0) continue;
-      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      if (bout) {
-        uint4* p = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + base + n);
-        if (g.accumulate) {
-          const uint4 o = *p;
-          const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+    for (int i0 = 0; i0 < NIT; i0 += CH) {
+      float v[CH][8];
+      long long off[CH];
+      bool ok[CH];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            v[2 * k] += __uint_as_float(w[k] << 16);
-            v[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
-          }
-        }
-        uint32_t w[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16);
-        *p = make_uint4(w[0], w[1], w[2], w[3]);
-        if (bnp) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {   // the values as stored
-            v[2 * k] = __uint_as_float(w[k] << 16);
-            v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
-          }
-        }
-      } else {
-        float4* p = reinterpret_cast<float4*>(C + base + n);
-        if (!split && g.accumulate) {
-          const float4 o0 = p[0], o1 = p[1];
-          v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w;
-          v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
-        }
-        p[0] = make_float4(v[0], v[1], v[2], v[3]);
-        p[1] = make_float4(v[4], v[5], v[6], v[7]);
+      for (int k = 0; k < CH; ++k) {
+        const int e = (i0 + k) * 64 + lane;
+        const int row = e / LPR, c8 = (e - row * LPR) * 8;
+        const float4 v0 = *reinterpret_cast<const float4*>(stage + row * S + c8);
+        const float4 v1 = *reinterpret_cast<const float4*>(stage + row * S + c8 + 4);
+        v[k][0] = v0.x; v[k][1] = v0.y; v[k][2] = v0.z; v[k][3] = v0.w;
+        v[k][4] = v1.x; v[k][5] = v1.y; v[k][6] = v1.z; v[k][7] = v1.w;
+        const int m = mw0 + i * 32 + row, n = nw0 + c8;
+        ok[k] = m < g.M && n < g.N;
+        const long long base = ok[k] ? (split ? (long long)m * g.N : out_row<OP>(g, m)) : 0;
+        ok[k] = ok[k] && base >= 0;
+        off[k] = ok[k] ? base + n : 0;     // element offset of the 8-vector in C (0: a safe dummy)
       }
-      if (bnp) {   // final values back into the stage for the column pass
-        *reinterpret_cast<float4*>(stage + row * S + c8) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(stage + row * S + c8 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      if (g.accumulate && !split) {        // uniform
+        if (bout) {
+          uint4 o[CH];
+#pragma unroll
+          for (int k = 0; k < CH; ++k)
+            o[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(g.C) + off[k]);
+#pragma unroll
+          for (int k = 0; k < CH; ++k) {
+            const uint32_t w[4] = {o[k].x, o[k].y, o[k].z, o[k].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              v[k][2 * q] += __uint_as_float(w[q] << 16);
+              v[k][2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
+            }
+          }
+        } else {
+          float4 o0[CH], o1[CH];
+#pragma unroll
+          for (int k = 0; k < CH; ++k) {
+            const float4* p = reinterpret_cast<const float4*>(C + off[k]);
+            o0[k] = p[0];
+            o1[k] = p[1];
+          }
+#pragma unroll
+          for (int k = 0; k < CH; ++k) {
+            v[k][0] += o0[k].x; v[k][1] += o0[k].y; v[k][2] += o0[k].z; v[k][3] += o0[k].w;
+            v[k][4] += o1[k].x; v[k][5] += o1[k].y; v[k][6] += o1[k].z; v[k][7] += o1[k].w;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        if (!ok[k]) continue;
+        if (bout) {
+          uint32_t w[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) w[q] = (uint32_t)f2bf(v[k][2 * q]) | ((uint32_t)f2bf(v[k][2 * q + 1]) << 16);
+          *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(g.C) + off[k]) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+          float4* p = reinterpret_cast<float4*>(C + off[k]);
+          p[0] = make_float4(v[k][0], v[k][1], v[k][2], v[k][3]);
+          p[1] = make_float4(v[k][4], v[k][5], v[k][6], v[k][7]);
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (bnp) {
-      const int slot = g.bnp_p0 + (mw0 + i * 32) / 32;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if (sj[j] < 0) continue;            // wave-uniform
-        float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const bool ok = mw0 + i * 32 + row_of(r) < g.M;
-          const float dv = stage[row_of(r) * S + j * 32 + l31];
-          float x;
-          if constexpr (BF16K) x = __uint_as_float((uint32_t)xr[j][r] << 16);
-          else x = xr[j][r];
-          const float xh = __fmul_rn(__fsub_rn(x, pmu[j]), pis[j]);
-          const float gv = (ok && __fadd_rn(xh, pbe[j]) > 0.f) ? dv : 0.f;
-          s0 += gv;
-          s1 = fmaf(gv, xh, s1);
-        }
-        s0 += __shfl_xor(s0, 32, 64);
-        s1 += __shfl_xor(s1, 32, 64);
-        const int n = nw0 + j * 32 + l31;
-#pragma unroll
-        for (int q = 0; q < kMaxBnp; ++q) {
-          const BnpArg& sg = g.bnp[q];
-          if (q == sj[j] && lh == 0 && n < sg.c_hi) {
-            const long long k = sg.set_off + (n - sg.c_lo);
-            sg.part[k * g.bnp_P + slot] = (double)s0;
-            sg.part[(sg.set_c + k) * g.bnp_P + slot] = (double)s1;
-          }
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
   }
 }
 
@@ -506,147 +413,6 @@ __global__ void __launch_bounds__(256) k_splitk_reduce_stats(const float* __rest
       g.stats[(long long)(g.N + c0 + j) * P + blockIdx.x] = bm[j];
     }
   }
-}
-
-// DGRAD split-K reduce as the last writer of dx, with the BN-backward partials
-// of jr_conv2d_bwd_data_bnp (the epilogue's job when K is not split).  Block
-// (b, y) owns rows [b*R, (b+1)*R) of the phase and columns [1024 y, 1024 y +
-// 1024); thread (q, rr) one float4 column group and rows rr, rr + rpp, ....
-// Per element the slabs are summed in k_splitk_reduce's order for G z-lanes
-// (lane zg sums slabs zg, zg + G, ..., lane sums added in zg order), so dx is
-// bitwise that kernel's; per column the thread sums dy' and dy' * xhat of the
-// final values over its rows (fp32 for bf16, fp64 for fp32), and a fixed tree
-// over the row phases gives the block's partial at slot bnp_p0 + b.
-template <typename TO>
-__global__ void __launch_bounds__(256) k_splitk_reduce_bnp(const float* __restrict__ slab, int splits, int G,
-                                                           ConvArgs g, TO* out, int R) {
-  typedef typename std::conditional<sizeof(TO) == 2, float, double>::type PS;
-  __shared__ PS red[2][256][4];
-  const int cb = blockIdx.y * 1024;
-  const int tpr = min(1024, g.N - cb) >> 2;
-  const int rpp = 256 / tpr;
-  const int t = threadIdx.x;
-  const int q = t % tpr, rr = t / tpr;
-  const int c0 = cb + q * 4;
-  const int r0 = blockIdx.x * R, r1 = min(g.M, r0 + R);
-  int sgi = -1;
-#pragma unroll
-  for (int s = 0; s < kMaxBnp; ++s)
-    if (s < g.bnp_n && c0 >= g.bnp[s].c_lo && c0 < g.bnp[s].c_hi) sgi = s;
-  const void* raw = nullptr;
-  int rs = 0, k = 0, cv = 0;
-  float mu[4] = {0.f, 0.f, 0.f, 0.f}, is[4] = {0.f, 0.f, 0.f, 0.f}, be[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < kMaxBnp; ++s) {
-    const BnpArg& sg = g.bnp[s];
-    if (s == sgi) {
-      k = c0 - sg.c_lo;
-      raw = static_cast<const TO*>(sg.raw) + sg.raw_off + k;
-      rs = sg.raw_stride;
-      cv = min(4, sg.c_hi - c0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (j < cv) { mu[j] = sg.mean[k + j]; is[j] = sg.invstd[k + j]; be[j] = sg.beta[k + j]; }
-    }
-  }
-  PS a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0};
-  if (rr < rpp) {
-    const long long zs = g.slab_elems >> 2;
-    for (int m = r0 + rr; m < r1; m += rpp) {
-      const float4* src = reinterpret_cast<const float4*>(slab + (long long)m * g.N + c0);
-      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int zg = 0; zg < G; ++zg) {
-        float4 l = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int z = zg; z < splits; z += G) {
-          const float4 a = src[z * zs];
-          l.x += a.x; l.y += a.y; l.z += a.z; l.w += a.w;
-        }
-        if (zg == 0) s = l;
-        else { s.x += l.x; s.y += l.y; s.z += l.z; s.w += l.w; }
-      }
-      const long long pix = dgrad_pix(g, m);
-      TO* p = out + pix * g.c_stride + g.c_off + c0;
-      float v[4];
-      if constexpr (sizeof(TO) == 4) {
-        float4* p4 = reinterpret_cast<float4*>(p);
-        if (g.accumulate) {
-          const float4 o = *p4;
-          s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
-        }
-        *p4 = s;
-        v[0] = s.x; v[1] = s.y; v[2] = s.z; v[3] = s.w;
-      } else {
-        uint2* p2 = reinterpret_cast<uint2*>(p);
-        if (g.accumulate) {
-          const uint2 o = *p2;
-          s.x += bf2f(o.x & 0xffff); s.y += bf2f(o.x >> 16); s.z += bf2f(o.y & 0xffff); s.w += bf2f(o.y >> 16);
-        }
-        const uint16_t b0 = f2bf(s.x), b1 = f2bf(s.y), b2 = f2bf(s.z), b3 = f2bf(s.w);
-        *p2 = make_uint2((uint32_t)b0 | ((uint32_t)b1 << 16), (uint32_t)b2 | ((uint32_t)b3 << 16));
-        v[0] = bf2f(b0); v[1] = bf2f(b1); v[2] = bf2f(b2); v[3] = bf2f(b3);
-      }
-      if (sgi < 0) continue;
-      float x[4];
-      if constexpr (sizeof(TO) == 4) {
-        const float4 xr = *reinterpret_cast<const float4*>(static_cast<const float*>(raw) + pix * rs);
-        x[0] = xr.x; x[1] = xr.y; x[2] = xr.z; x[3] = xr.w;
-      } else {
-        const uint2 xr = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(raw) + pix * rs);
-        x[0] = bf2f(xr.x & 0xffff); x[1] = bf2f(xr.x >> 16); x[2] = bf2f(xr.y & 0xffff); x[3] = bf2f(xr.y >> 16);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float xh = __fmul_rn(__fsub_rn(x[j], mu[j]), is[j]);
-        const float gv = (j < cv && __fadd_rn(xh, be[j]) > 0.f) ? v[j] : 0.f;
-        if constexpr (sizeof(TO) == 2) {
-          a0[j] += gv;
-          a1[j] = fmaf(gv, xh, a1[j]);
-        } else {
-          a0[j] += (double)gv;
-          a1[j] += (double)gv * (double)xh;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) { red[0][t][j] = a0[j]; red[1][t][j] = a1[j]; }
-  __syncthreads();
-  int span = 1;
-  while (span < rpp) span <<= 1;
-  for (int h = span >> 1; h > 0; h >>= 1) {
-    if (rr < h && rr + h < rpp) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        red[0][t][j] += red[0][t + h * tpr][j];
-        red[1][t][j] += red[1][t + h * tpr][j];
-      }
-    }
-    __syncthreads();
-  }
-  if (rr != 0 || sgi < 0) return;
-  const int slot = g.bnp_p0 + blockIdx.x;
-#pragma unroll
-  for (int s = 0; s < kMaxBnp; ++s) {
-    const BnpArg& sg = g.bnp[s];
-    if (s == sgi) {
-      for (int j = 0; j < cv; ++j) {
-        const long long kk = sg.set_off + k + j;
-        sg.part[kk * g.bnp_P + slot] = (double)red[0][t][j];
-        sg.part[(sg.set_c + kk) * g.bnp_P + slot] = (double)red[1][t][j];
-      }
-    }
-  }
-}
-
-// Row blocks of k_splitk_reduce_bnp / k_splitk_reduce_stats: R rows each
-// (a multiple of the rows one pass of 256 threads covers), ~512 blocks.
-static inline void reduce_rows(int M, int N, int* R, int* P) {
-  const int rpp = 256 / ((N < 1024 ? N : 1024) / 4);
-  int r = (M + 511) / 512;
-  r = r > rpp ? r : rpp;
-  r = (r + rpp - 1) / rpp * rpp;
-  *R = r;
-  *P = (M + r - 1) / r;
 }
 
 // (mean, invstd) per channel from stats[2][N][P] partials of R rows each

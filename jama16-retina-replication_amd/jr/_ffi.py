@@ -50,14 +50,6 @@ class BnSeg(Structure):
                 ("beta", c_void_p), ("dbeta", c_void_p)]
 
 
-class BnpSeg(Structure):
-    """include/jr.h jr_bnp_seg: one BN layer's dx channel slice whose backward partial
-    sums the data-gradient epilogue writes (jr_conv2d_bwd_data_bnp)."""
-    _fields_ = [("raw", c_void_p), ("mean", c_void_p), ("invstd", c_void_p), ("beta", c_void_p),
-                ("part", c_void_p)] + [(n, c_int32) for n in (
-                    "c_lo", "c_hi", "raw_c_off", "raw_c_stride", "set_c", "set_off")]
-
-
 class WgradSeg(Structure):
     """include/jr.h jr_wgrad_seg: one layer of the deferred filter-gradient reduce."""
     _fields_ = [("slabs", c_void_p), ("dw", c_void_p)] + [(n, c_int32) for n in (
@@ -81,9 +73,6 @@ _SIGS = {
                                        c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_bwd_data": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_int,
                                    c_void_p, c_size_t, c_void_p]),
-    "jr_conv2d_bwd_data_bnp_slots": (c_int, [POINTER(ConvDesc), c_int, POINTER(c_int32)]),
-    "jr_conv2d_bwd_data_bnp": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                                       c_void_p, c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_bwd_filter": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_wgrad_seg": (c_int, [POINTER(ConvDesc), c_int, POINTER(WgradSeg)]),
@@ -123,9 +112,6 @@ _SIGS = {
                                c_size_t, c_void_p]),
     "jr_bn_relu_bwd_multi": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int32,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
-    "jr_bn_relu_bwd_parts": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_int32,
-                                     c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
-                                     c_void_p]),
     "jr_maxpool3x3s2_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p,
                                     c_void_p]),
     "jr_maxpool3x3s2_bwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p, c_int,

@@ -65,7 +65,7 @@ class Engine:
                  optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
                  head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None,
                  autotune: bool = False, tiles: str = "pinned", fuse_siblings: bool = True, lanes: int = 2,
-                 conv_math: Optional[str] = None, defer_wgrad: bool = True, bn_fuse: bool = False):
+                 conv_math: Optional[str] = None, defer_wgrad: bool = True):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if conv_math is None:            # fp32 default: x8 (fp32-accurate, on the bf16 matrix cores)
@@ -117,12 +117,6 @@ class Engine:
         # summed by ONE jr_wgrad_reduce launch per flush point (the end of the
         # backward, and each gradient bucket's issue point: set_flush_points)
         self.defer_wgrad = bool(defer_wgrad)
-        # bn_fuse: the BN backward's reduce pass runs in the epilogue of the
-        # data-gradient GEMM that writes a layer's upstream gradient last
-        # (jr_conv2d_bwd_data_bnp) wherever one such GEMM covers the whole
-        # launch set (_bn_fusion).  Off by default: measured neutral to slower
-        # on MI355X ("BN partials in the dgrad epilogue")
-        self.bn_fuse = bool(bn_fuse)
         self._flush_points: List[int] = []
         self._graphs: Dict[int, int] = {}
         self.bucket_hooks: List[Tuple[int, Callable]] = []
@@ -433,57 +427,6 @@ class Engine:
             groups = [[mc] for mc in groups[0]]
         return groups
 
-    def _bn_fusion(self, B: int, keep: list):
-        """Which BN backward launch sets take their reduce pass from a
-        data-gradient epilogue (jr_conv2d_bwd_data_bnp).  The backward visits
-        the nodes in reverse, so the LAST writer of a buffer's gradient is the
-        consumer visited last; a set qualifies when every member's buffer has
-        the same last writer, a conv launch whose planned dgrad does not split
-        K (jr_conv2d_bwd_data_bnp_slots) and that covers at most 6 slices.
-        Returns ({(uid, set index): (partials, P)}, {writer uid: [(BnpSeg, key)]})."""
-        L, g = self.lib, self.g
-        unit_of = self.plan.unit_of
-        last = {}
-        for n in reversed(g.nodes):
-            if n.kind == "conv":
-                u = unit_of[n.idx]
-                if u.first is not n:
-                    continue
-            last[n.x] = n
-        slots: Dict[int, Optional[int]] = {}
-        sets, writers = {}, {}
-        for u in self.cunits:
-            uid = u.first.idx
-            for gi, grp in enumerate(self._bn_groups(u)):
-                ws_ = {id(last.get(m.y.buf)) for m, _ in grp}
-                f = last.get(grp[0][0].y.buf)
-                if len(ws_) != 1 or f is None or f.kind != "conv":
-                    continue
-                fu = unit_of[f.idx]
-                fid = fu.first.idx
-                if fid not in slots:
-                    d = self._conv_desc(fu, B)
-                    keep.append(d)
-                    P = ctypes.c_int32(0)
-                    rc = L.jr_conv2d_bwd_data_bnp_slots(ctypes.byref(d), self.cdt, ctypes.byref(P))
-                    slots[fid] = P.value if rc == 0 and P.value > 0 else None
-                P = slots[fid]
-                if P is None or len(writers.get(fid, [])) + len(grp) > 6:
-                    continue
-                co0 = grp[0][1]
-                cg = sum(m.cout for m, _ in grp)
-                part = torch.zeros(2 * cg * P, dtype=torch.float64, device=self.device)
-                keep.append(part)
-                key = (uid, gi)
-                sets[key] = (part, P)
-                for m, co in grp:
-                    seg = _ffi.BnpSeg(self.raw_unit[uid].data_ptr(), self.mean_unit[uid].data_ptr() + 4 * co,
-                                      self.invstd_unit[uid].data_ptr() + 4 * co,
-                                      self._p(f"batch_normalization_{m.idx + 1}/beta"), part.data_ptr(),
-                                      m.y.c_off, m.y.c_off + m.cout, co, u.cout, cg, co - co0)
-                    writers.setdefault(fid, []).append((seg, key))
-        return sets, writers
-
     def _build_calls(self, B: int, nl: Optional[int] = None, one_stream: bool = False):
         """Pre-bound Calls (jr.lanes) for forward, backward, update on nl
         lanes (default self.nlanes), with their cross-lane waits:
@@ -605,8 +548,6 @@ class Engine:
                 self.slab_bytes = off
             pending: List[Tuple[_ffi.WgradSeg, int]] = []
             flush_at = list(self._flush_points)
-            bnp_sets, bnp_writers = self._bn_fusion(B, keep) if self.bn_fuse else ({}, {})
-            self.bn_fused_sets = len(bnp_sets)
 
             def flush():
                 """One jr_wgrad_reduce over every pending layer (lane 0)."""
@@ -647,10 +588,8 @@ class Engine:
                     raw = self.raw_unit[uid].data_ptr()
                     draw = self.draw_lane[ln].data_ptr()
                     # one backward launch set for all members of the launch (segments:
-                    # each member's upstream gradient slice, beta and dbeta); its
-                    # reduce pass already ran where a data-gradient epilogue wrote
-                    # the partial sums (bnp_sets)
-                    for gi, grp in enumerate(self._bn_groups(u)):
+                    # each member's upstream gradient slice, beta and dbeta)
+                    for grp in self._bn_groups(u):
                         co0 = grp[0][1]
                         cg = sum(m.cout for m, _ in grp)
                         segs = (_ffi.BnSeg * len(grp))(*[
@@ -658,19 +597,12 @@ class Engine:
                                        self._p(f"batch_normalization_{m.idx + 1}/beta"),
                                        self._gp(f"batch_normalization_{m.idx + 1}/beta")) for m, _ in grp])
                         keep.append(segs)
-                        reads = [("d", m.y.buf, m.y.c_off) for m, _ in grp] + [("r", uid), ("p",)]
-                        mu, isd = self.mean_unit[uid].data_ptr() + 4 * co0, self.invstd_unit[uid].data_ptr() + 4 * co0
-                        if (uid, gi) in bnp_sets:
-                            part, P = bnp_sets[(uid, gi)]
-                            add(bwd, L.jr_bn_relu_bwd_parts, (dt, len(grp), ctypes.byref(segs), part.data_ptr(), P,
-                                                              raw, co0, u.cout, M, cg, mu, isd, draw, ws, wsb, s),
-                                "bn_relu_bwd", ln, reads + [("bnp", uid, gi)], [("draw", ln), ("g", uid), ("ws", ln)],
-                                nbytes=3 * M * cg * self.esz)
-                        else:
-                            add(bwd, L.jr_bn_relu_bwd_multi, (dt, len(grp), ctypes.byref(segs), raw, co0, u.cout, M,
-                                                              cg, mu, isd, draw, ws, wsb, s),
-                                "bn_relu_bwd", ln, reads, [("draw", ln), ("g", uid), ("ws", ln)],
-                                nbytes=3 * M * cg * self.esz)
+                        add(bwd, L.jr_bn_relu_bwd_multi, (dt, len(grp), ctypes.byref(segs), raw, co0, u.cout, M, cg,
+                                                          self.mean_unit[uid].data_ptr() + 4 * co0,
+                                                          self.invstd_unit[uid].data_ptr() + 4 * co0, draw, ws, wsb,
+                                                          s),
+                            "bn_relu_bwd", ln, [("d", m.y.buf, m.y.c_off) for m, _ in grp] + [("r", uid), ("p",)],
+                            [("draw", ln), ("g", uid), ("ws", ln)], nbytes=3 * M * cg * self.esz)
                     dkey = ("draw", ln)
                     if x8p:             # the raw-output gradient as split planes (dgrad and wgrad operand)
                         drawp = self.drawp_lane[ln].data_ptr()
@@ -687,19 +619,9 @@ class Engine:
                                                           self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
                             "conv_wgrad", ln, ax_reads(u.x) + [dkey], [("g", uid), ("ws", ln)])
                     if u.x != g.input_buf:
-                        bsegs = bnp_writers.get(uid)
-                        if bsegs:       # the last writer of dx: BN partials of the producers' sets too
-                            arr = (_ffi.BnpSeg * len(bsegs))(*[sg for sg, _ in bsegs])
-                            keep.append(arr)
-                            keys = sorted({k for _, k in bsegs})
-                            add(bwd, L.jr_conv2d_bwd_data_bnp, (ctypes.byref(d), cdt, draw, self._wd(u), D(u.x), acc,
-                                                                len(bsegs), ctypes.byref(arr), ws, wsb, s),
-                                "conv_dgrad", ln, [dkey, wkey, ("p",)] + [("r", k[0]) for k in keys],
-                                d_all(u.x) + [("ws", ln)] + [("bnp",) + k for k in keys])
-                        else:
-                            add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), cdt, draw, self._wd(u), D(u.x), acc, ws,
-                                                            wsb, s),
-                                "conv_dgrad", ln, [dkey, wkey], d_all(u.x) + [("ws", ln)])
+                        add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), cdt, draw, self._wd(u), D(u.x), acc, ws, wsb,
+                                                        s),
+                            "conv_dgrad", ln, [dkey, wkey], d_all(u.x) + [("ws", ln)])
                         written.add(u.x)
                     trigger = False
                     while flush_at and flush_at[0] >= u.koff:
