@@ -36,6 +36,10 @@ template <int MODE> constexpr int red_rows() { return MODE == 0 ? 16 : JR_BN_BWD
 #endif
 constexpr int kAppUnroll = JR_BN_APP_UNROLL;  // rows per thread in the elementwise passes
 
+// Pins a loaded vector in registers at this point: hipcc otherwise sinks a
+// load into the conditional block of its only use (one wait per row).
+__device__ __forceinline__ void pin(uint4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
 // Same rounding in fwd and bwd so the ReLU mask is bit-identical.
 __device__ __forceinline__ float bn_xhat(float x, float mean, float invstd) {
   return __fmul_rn(__fsub_rn(x, mean), invstd);
@@ -331,19 +335,25 @@ __global__ void __launch_bounds__(256) k_bn_relu_apply(const T* __restrict__ x, 
     mu[j] = mean[q * VW + j]; is[j] = invstd[q * VW + j]; be[j] = beta[q * VW + j];
   }
   const int64_t r0 = (int64_t)blockIdx.x * rpp * kAppUnroll + rr;
-  float xv[kAppUnroll][VW];
+  // every row's load is unconditional (rows past m re-read row m - 1) and
+  // unpacked only after all were issued: a load under `if (r < m)` whose
+  // bf16 unpack sat in the same branch made hipcc wait for each row in turn
+  uint4 xr[kAppUnroll];
 #pragma unroll
   for (int u = 0; u < kAppUnroll; ++u) {
-    const int64_t r = r0 + (int64_t)u * rpp;
-    if (r < m) Vec<T>::ld(x + r * xs + q * VW, xv[u]);
+    const int64_t r = min(r0 + (int64_t)u * rpp, m - 1);
+    xr[u] = *reinterpret_cast<const uint4*>(x + r * xs + q * VW);
   }
+#pragma unroll
+  for (int u = 0; u < kAppUnroll; ++u) pin(xr[u]);
 #pragma unroll
   for (int u = 0; u < kAppUnroll; ++u) {
     const int64_t r = r0 + (int64_t)u * rpp;
     if (r >= m) break;
-    float o[VW];
+    float xv[VW], o[VW];
+    Vec<T>::unpack(xr[u], xv);
 #pragma unroll
-    for (int j = 0; j < VW; ++j) o[j] = fmaxf(bn_pre(xv[u][j], mu[j], is[j], be[j]), 0.f);
+    for (int j = 0; j < VW; ++j) o[j] = fmaxf(bn_pre(xv[j], mu[j], is[j], be[j]), 0.f);
     Vec<T>::st(y + r * y_stride + y_off + q * VW, o);
   }
 }
@@ -370,25 +380,32 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(BnSegs sg, const T* _
     mu[j] = mean[k]; is[j] = invstd[k]; be[j] = sg.beta[sgi][lc + j]; c1[j] = k1[k]; c2[j] = k2[k];
   }
   const int64_t r0 = (int64_t)blockIdx.x * rpp * kAppUnroll + rr;
-  float xv[kAppUnroll][VW], gv[kAppUnroll][VW];
+  // unconditional loads (rows past m re-read row m - 1), unpacked after all
+  // were issued (as in k_bn_relu_apply)
+  uint4 xr[kAppUnroll], gr[kAppUnroll];
 #pragma unroll
   for (int u = 0; u < kAppUnroll; ++u) {
-    const int64_t r = r0 + (int64_t)u * rpp;
-    if (r < m) {
-      Vec<T>::ld(x + r * xs + q * VW, xv[u]);
-      Vec<T>::ld(dy + r * dy_stride, gv[u]);
-    }
+    const int64_t r = min(r0 + (int64_t)u * rpp, m - 1);
+    xr[u] = *reinterpret_cast<const uint4*>(x + r * xs + q * VW);
+    gr[u] = *reinterpret_cast<const uint4*>(dy + r * dy_stride);
+  }
+#pragma unroll
+  for (int u = 0; u < kAppUnroll; ++u) {
+    pin(xr[u]);
+    pin(gr[u]);
   }
 #pragma unroll
   for (int u = 0; u < kAppUnroll; ++u) {
     const int64_t r = r0 + (int64_t)u * rpp;
     if (r >= m) break;
-    float o[VW];
+    float xv[VW], gv[VW], o[VW];
+    Vec<T>::unpack(xr[u], xv);
+    Vec<T>::unpack(gr[u], gv);
 #pragma unroll
     for (int j = 0; j < VW; ++j) {
-      const float xh = bn_xhat(xv[u][j], mu[j], is[j]);
+      const float xh = bn_xhat(xv[j], mu[j], is[j]);
       const float pre = __fadd_rn(xh, be[j]);
-      const float g = pre > 0.f ? gv[u][j] : 0.f;
+      const float g = pre > 0.f ? gv[j] : 0.f;
       o[j] = is[j] * (g - c1[j] - xh * c2[j]);
     }
     Vec<T>::st(dx + r * xs + q * VW, o);
