@@ -56,7 +56,10 @@ def parse():
     ap.add_argument("--conv-math", default="x8", choices=["f32", "x8", "x8p"],
                     help="dtype f32 only. x8 (default): fp32 tensors, products from an exact 3-way bf16 split "
                          "(jr.h JR_F32_X8, fp32-accurate); f32: fp32 MFMA")
-    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a HIP graph")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay a HIP graph of the step instead of eager launches (round 2: eager on two lanes "
+                         "measured 1.3-1.5%% faster, profiles/r02c_graph_ab.txt)")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches (the default; kept for old commands)")
     ap.add_argument("--lanes", type=int, default=2, help="streams for branch-level concurrency (jr.lanes)")
     ap.add_argument("--tiles", default="pinned", choices=["pinned", "heuristic", "autotune"],
                     help="conv tiles: the committed MI355X table of this workload (train.py's default; "
@@ -266,7 +269,7 @@ def main():
     eng.synchronize()
     log(f"engine ready (rank {rank}/{world})")
     ar = BucketAllReduce(eng, world) if world > 1 and train else None
-    use_graph = (not args.no_graph) and ar is None and args.lanes <= 2   # graphs: at most two lanes (jr.engine.capture)
+    use_graph = args.graph and not args.no_graph and ar is None and args.lanes <= 2   # graphs: at most two lanes
 
     def step():
         if use_graph:
