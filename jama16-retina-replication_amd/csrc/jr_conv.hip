@@ -622,10 +622,19 @@ static int chan_pad(int c, int dtype) {
 static int std_count(int dtype) {
   return dtype == JR_BF16 ? kNumCfgsBf16 : dtype == JR_F32_X8P ? kNumCfgsX8P : kNumCfgs;
 }
-static int cfg_count(int dtype) { return std_count(dtype) + (dtype == JR_BF16 ? kNumHaloBf16 : 0); }
+// JR_F32_X8 also selects the fp32-MFMA kernel of every fp32 tile (ids
+// kNumCfgs + t): both are fp32-accurate, and on the stem's N = 32 / 64
+// filter-gradient GEMMs, whose per-wave split VALU outweighs the 8-product
+// MFMA gain, the fp32 MFMA is the faster one -- autotuning and the pinned
+// tables choose per GEMM (the planner heuristic keeps x8).
+static int cfg_count(int dtype) {
+  return std_count(dtype) + (dtype == JR_BF16 ? kNumHaloBf16 : dtype == JR_F32_X8 ? kNumCfgs : 0);
+}
 static bool is_halo(int dtype, int tile) { return dtype == JR_BF16 && tile >= kNumCfgsBf16; }
+static bool is_x8_f32(int dtype, int tile) { return dtype == JR_F32_X8 && tile >= kNumCfgs; }
 static const TileCfg& tile_cfg(int dtype, int tile) {
   if (is_halo(dtype, tile)) return kHaloBf16[tile - kNumCfgsBf16].t;
+  if (is_x8_f32(dtype, tile)) return kCfgs[tile - kNumCfgs];
   return (dtype == JR_BF16 ? kCfgsBf16 : dtype == JR_F32_X8P ? kCfgsX8P : kCfgs)[tile];
 }
 // Halo rows a BM-row tile needs: output rows it spans (bound) + kh - 1.
@@ -873,6 +882,8 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     const TileCfg& t = tile_cfg(dtype, p.tile);
     const bool fast = OP == OP_WGRAD ? a.wo >= t.bk : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
     launch_conv_bf16(OP, p.tile, fast, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
+  } else if (is_x8_f32(dtype, p.tile)) {
+    launch_op<OP>(p.tile - kNumCfgs, a, grid, s);     // the fp32-MFMA kernel of that tile
   } else if (dtype == JR_F32_X8) {
     launch_op<OP, 0, true>(p.tile, a, grid, s);
   } else {
