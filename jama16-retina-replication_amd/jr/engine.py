@@ -98,11 +98,16 @@ class Engine:
         self.adam_b1, self.adam_b2, self.adam_eps, self.adam_t = 0.9, 0.999, 1e-8, 0
         self.head_mode = _ffi.JR_HEAD_SIGMOID if head == "sigmoid" else _ffi.JR_HEAD_SOFTMAX
         self.units = self.g.units
-        self.stream = torch.cuda.Stream(device=self.device)
+        # (diagnostic) JR_LANE_PRIORITY="p0,p1,...": HIP stream priority per lane
+        # (lower = higher priority); default: all normal
+        prio = [int(v) for v in os.environ.get("JR_LANE_PRIORITY", "").split(",") if v.strip()]
+        prio += [0] * max(0, int(lanes) - len(prio))
+        self.stream = torch.cuda.Stream(device=self.device, priority=prio[0])
         self._s = ctypes.c_void_p(self.stream.cuda_stream)
         # lanes (jr.lanes): lane 0 is self.stream, where every step starts and ends
         self.nlanes = max(1, int(lanes))
-        self.lane_streams = [self.stream] + [torch.cuda.Stream(device=self.device) for _ in range(self.nlanes - 1)]
+        self.lane_streams = [self.stream] + [torch.cuda.Stream(device=self.device, priority=prio[i])
+                                             for i in range(1, self.nlanes)]
         self._fork_ev = torch.cuda.Event()
         self._join_ev = [torch.cuda.Event() for _ in range(self.nlanes - 1)]
         self._tail_ev = [torch.cuda.Event() for _ in range(self.nlanes)]

@@ -56,7 +56,8 @@ def test_validation_errors_without_gpu():
     assert L.jr_conv2d_workspace_size(None, 0, 0) == 0
     # JR_F32_X8 (dtype 2): fp32 storage rules and tile table, conv entry points only
     d = _ffi.ConvDesc(2, 17, 17, 64, 96, 3, 3, 1, 1, 1, 1, 17, 17, 0, 64, 0, 96)
-    assert L.jr_conv2d_num_configs(2) == L.jr_conv2d_num_configs(0) > 0
+    # (x8 ids 0-13: the split kernel; 14-27: the fp32-MFMA kernel of the same tiles)
+    assert L.jr_conv2d_num_configs(2) == 2 * L.jr_conv2d_num_configs(0) > 0
     for op in range(3):
         assert L.jr_conv2d_workspace_size(ctypes.byref(d), op, 2) == L.jr_conv2d_workspace_size(ctypes.byref(d), op, 0)
     # JR_F32_X8P (dtype 3): bf16-operand channel rules (radix 8), its own tile table
