@@ -761,7 +761,10 @@ static void stats_geom(int dtype, const Plan& p, int* P, int* R) {
 
 static size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
-constexpr int kStatsChunk = 4096;   // partials one finalize block combines
+#ifndef JR_STATS_CHUNK
+#define JR_STATS_CHUNK 4096
+#endif
+constexpr int kStatsChunk = JR_STATS_CHUNK;   // partials one finalize block combines
 
 static size_t stats_ws(int dtype, const Plan& p) {
   int P, R;

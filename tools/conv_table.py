@@ -33,11 +33,24 @@ def phases(u):
     return k
 
 
-seq = [(u, "fwd", 2 * u.macs_per_image() * B) for u in plan.units]
+# plan order: the forward GEMMs, then per unit in reverse its backward group
+# (filter gradient + data-gradient phases, in whatever order the engine issues
+# them: matched below by the OP template argument of the kernel name)
+groups = [[(u, "fwd", 2 * u.macs_per_image() * B)] for u in plan.units]
 for u in reversed(plan.units):
-    seq.append((u, "wgrad", 2 * u.macs_per_image() * B))
+    grp = [(u, "wgrad", 2 * u.macs_per_image() * B)]
     if u.x != g.input_buf:
-        seq += [(u, op, f) for op, f in phases(u)]
+        grp += [(u, op, f) for op, f in phases(u)]
+    groups.append(grp)
+seq = [e for grp in groups for e in grp]
+
+
+def op_of(name):
+    """0 fwd / 1 dgrad / 2 wgrad from the kernel name (halo kernels: fwd)."""
+    if "k_conv_halo<" in name:
+        return 0
+    a = name[name.index("<") + 1:]
+    return int(a.split(",")[0].split(">")[0].strip())
 
 opt = [i for i, r in enumerate(rows) if "k_nesterov" in r["Kernel_Name"] or "k_sgd" in r["Kernel_Name"]]
 step_rows = rows[opt[-2] + 1:opt[-1] + 1] if len(opt) >= 2 else rows
@@ -47,7 +60,7 @@ i = 0
 while i < len(step_rows):
     r = step_rows[i]
     nm = r["Kernel_Name"]
-    if ("k_conv<" in nm or "k_conv_bf16<" in nm):
+    if ("k_conv<" in nm or "k_conv_bf16<" in nm or "k_conv_halo<" in nm):
         t = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         t2 = 0
         j = i + 1
@@ -61,16 +74,56 @@ while i < len(step_rows):
 if len(conv) != len(seq):
     print(f"warning: {len(conv)} conv GEMMs in the step, plan expects {len(seq)}", file=sys.stderr)
 last = conv[-len(seq):]
-tot_t = 0; tot_f = 0
+# within each backward group, give the filter gradient the OP=2 launch and
+# the data-gradient phases the OP=1 launches in issue order
+aligned, k = [], 0
+for grp in groups:
+    ks = last[k:k + len(grp)]
+    k += len(grp)
+    w = [c for c in ks if op_of(c[0]["Kernel_Name"]) == 2]
+    d = [c for c in ks if op_of(c[0]["Kernel_Name"]) == 1]
+    f = [c for c in ks if op_of(c[0]["Kernel_Name"]) == 0]
+    for (u, op, fl) in grp:
+        src = f if op == "fwd" else w if op == "wgrad" else d
+        if not src:
+            print(f"warning: no OP match for {u.name} {op}", file=sys.stderr)
+            src = [c for c in (f, w, d) if c][0]
+        aligned.append(src.pop(0))
+last = aligned
+# per-call floor: max(flops at the dense bf16 MFMA peak, compulsory HBM bytes
+# at 8 TB/s) -- bf16 kernels only (fp32 kernels: the x8 / fp32-MFMA peaks differ)
+PEAK_TF, PEAK_GBS = 2500.0, 8000.0
+
+
+def floor_us(u, op, f, name):
+    if "bf16" not in name and "halo" not in name:
+        return None
+    e = 2   # bytes per bf16 element
+    x = B * u.h * u.w * u.cin * e
+    y = B * u.ho * u.wo * u.cout * e
+    wt = u.kh * u.kw * u.cin * u.cout * e
+    byts = {"fwd": x + y + wt, "wgrad": x + y + 2 * wt}.get(op, y + x + wt)   # dgrad phases: dy + dx + w
+    if op.startswith("dg") and op != "dgrad":
+        byts /= u.stride * u.stride
+    return max(f / PEAK_TF / 1e6, byts / PEAK_GBS / 1e3)
+
+
+tot_t = 0; tot_f = 0; tot_floor = 0.0
 out = []
 for (u, op, f), (r, t, t2) in zip(seq, last):
     tot_t += t + t2; tot_f += f
     name = r["Kernel_Name"]; cfg = name[name.index("<"):name.index(">") + 1]
+    fl = floor_us(u, op, f, name)
+    tot_floor += fl or 0.0
+    ftxt = f"  floor {fl:6.1f}us ({fl * 1e3 / max(t + t2, 1):4.2f})" if fl is not None else ""
     out.append((t + t2, f"{u.name:14s} {op:5s} {u.kh}x{u.kw}/{u.stride} {u.h:3d}x{u.w:<3d} {u.cin:4d}->{u.cout:4d} "
-                f"{cfg:24s} grid={r['Grid_Size_X']:>7s}x{r['Grid_Size_Z']:<4s} {t/1e3:8.1f}+{t2/1e3:6.1f}us {f/max(t+t2, 1)/1e3:7.1f} TF/s"))
+                f"{cfg:24s} grid={r['Grid_Size_X']:>7s}x{r['Grid_Size_Z']:<4s} {t/1e3:8.1f}+{t2/1e3:6.1f}us {f/max(t+t2, 1)/1e3:7.1f} TF/s"
+                + ftxt))
 for t, s in sorted(out, reverse=True)[:int(sys.argv[3]) if len(sys.argv) > 3 else 40]:
     print(s)
-print(f"total conv {tot_t/1e6:.2f} ms, {tot_f/max(tot_t, 1)/1e3:.1f} TF/s")
+print(f"total conv {tot_t/1e6:.2f} ms, {tot_f/max(tot_t, 1)/1e3:.1f} TF/s"
+      + (f"; sum of per-call floors {tot_floor/1e3:.2f} ms ({tot_floor*1e3/max(tot_t, 1):.2f} of the time)"
+         if tot_floor else ""))
 
 # ---- whole-step breakdown: kernels between the last two optimizer launches
 opt = [i for i, r in enumerate(rows) if "k_nesterov" in r["Kernel_Name"] or "k_sgd" in r["Kernel_Name"]]
