@@ -146,6 +146,33 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(jr_pool_desc d, const uint8
 #endif
 constexpr int kStrip = JR_POOL_STRIP;
 
+// x / d for a tap count d = ch * cw in {1, 2, 3, 4, 6, 9}, bitwise the IEEE
+// division without its ~10-instruction sequence: q = x * RN(1/d) and one
+// fma correction, guarded for q = +-0 / +-inf / NaN (selects) and for
+// |x| < 2^-100 (x / 6 subnormal: one-ulp misses there), where a vector with
+// any such component takes the true division (one branch per vector).
+// Exhaustively verified over all 2^32 inputs per d (tools/verify_pool_div.c).
+// The backward divides every dy element 3 (kStrip + 2) / kStrip times.
+__device__ __forceinline__ float tap_recip(float d) {
+  return d == 9.f ? 0x1.c71c72p-4f : d == 6.f ? 0x1.555556p-3f : d == 4.f ? 0.25f
+       : d == 3.f ? 0x1.555556p-2f : d == 2.f ? 0.5f : 1.f;
+}
+__device__ __forceinline__ float pool_div(float x, float d, float r) {
+  const float q = __fmul_rn(x, r);
+  const float c = __builtin_fmaf(__builtin_fmaf(-q, d, x), r, q);
+  return (q == 0.f || !__builtin_isfinite(q)) ? q : c;
+}
+__device__ __forceinline__ float4 pool_div4(float4 v, float d) {
+#ifdef JR_POOL_TRUE_DIV   // A/B: the IEEE division sequence
+  return make_float4(v.x / d, v.y / d, v.z / d, v.w / d);
+#endif
+  // one branch per vector: any |component| < 2^-100 takes the true division
+  const float m = fminf(fminf(fabsf(v.x), fabsf(v.y)), fminf(fabsf(v.z), fabsf(v.w)));
+  if (__builtin_expect(m < 0x1p-100f, 0)) return make_float4(v.x / d, v.y / d, v.z / d, v.w / d);
+  const float r = tap_recip(d);
+  return make_float4(pool_div(v.x, d, r), pool_div(v.y, d, r), pool_div(v.z, d, r), pool_div(v.w, d, r));
+}
+
 template <typename T, bool BWD>
 __device__ __forceinline__ float4 box_row(const jr_pool_desc& d, const T* __restrict__ src, int b, int h, int w,
                                           int q) {
@@ -161,7 +188,7 @@ __device__ __forceinline__ float4 box_row(const jr_pool_desc& d, const T* __rest
     float4 v = P4<T>::ld(src + ((int64_t)(b * d.h + h) * d.w + iw) * stride + off + q * 4);
     if (BWD) {
       const float fc = (float)(ch * (1 + (iw > 0) + (iw < d.w - 1)));
-      v = make_float4(v.x / fc, v.y / fc, v.z / fc, v.w / fc);
+      v = pool_div4(v, fc);
     }
     s = f4add(s, v);
   }
@@ -190,7 +217,7 @@ __global__ void __launch_bounds__(256) k_avgpool_box(jr_pool_desc d, const T* __
       float4 o = f4add(f4add(up, mid), dn);
       if (!BWD) {
         const float fc = (float)((1 + (h > 0) + (h < d.h - 1)) * (1 + (w > 0) + (w < d.w - 1)));
-        o = make_float4(o.x / fc, o.y / fc, o.z / fc, o.w / fc);
+        o = pool_div4(o, fc);
       }
       const int ostride = BWD ? d.x_c_stride : d.y_c_stride;
       const int ooff = BWD ? d.x_c_off : d.y_c_off;
