@@ -135,7 +135,11 @@ int jr_conv2d_bwd_filter(const jr_conv_desc* d, int dtype, const void* x, const 
  * ONE launch, bitwise equal to jr_conv2d_bwd_filter's own reduce.  segs is
  * a DEVICE array; each entry is filled by jr_conv2d_wgrad_seg (geometry,
  * lanes g, blocks) plus the caller's slabs / dw pointers and block0 = the
- * exclusive prefix sum of blocks (total_blocks = the sum). */
+ * exclusive prefix sum of blocks (total_blocks = the sum).  slab_bytes must
+ * EQUAL the segment's splits * m * n * 4: a plan whose split count changed
+ * since the segment was filled (another set_config / autotune on the same
+ * geometry) fails with JR_ERR_INVALID instead of leaving stale slabs in the
+ * reduce. */
 typedef struct jr_wgrad_seg {
   const float* slabs;
   float* dw;
@@ -159,6 +163,11 @@ int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const void* a, 
 int jr_conv2d_get_config(const jr_conv_desc* d, int op, int dtype, int phase);
 int jr_conv2d_set_config(const jr_conv_desc* d, int op, int dtype, int phase, int cfg);
 int jr_conv2d_num_configs(int dtype);   /* tiles of that dtype's table */
+/* Process-wide counter, bumped whenever set_config or autotune CHANGES an
+ * override (re-setting an equal value does not): a caller that bound plans
+ * (e.g. deferred filter-gradient segments) re-applies its own configs when
+ * the generation moved since it did. */
+unsigned long long jr_conv2d_config_generation(void);
 
 /* ---- BatchNormalization(scale=False, eps) + ReLU, training-mode batch
  *      statistics (Keras conv2d_bn; App. C Q1: always batch stats) ----- */
@@ -313,13 +322,17 @@ int jr_example_parse_image(const uint8_t* base, const uint64_t* offsets, const u
  * per GPU), in-place sum of the flat gradient enqueued on the caller's
  * stream.  The 128-byte unique id comes from rank 0's jr_comm_unique_id and
  * reaches the other ranks through the caller's bootstrap, or through a file
- * (jr_comm_init_file: rank 0 writes it with an atomic rename, the others
- * poll up to timeout_ms, < 0 = forever). */
+ * (jr_comm_init_file: rank 0 writes it, tagged with run_id, with an atomic
+ * rename; the others poll up to timeout_ms, < 0 = forever, for the file of
+ * THEIR run_id, so an id an earlier job left at uid_path is never joined;
+ * run_id: any non-empty string every rank of one job shares, e.g. the
+ * launcher's rendezvous id). */
 #define JR_COMM_ID_BYTES 128
 typedef struct jr_comm jr_comm;
 int jr_comm_unique_id(uint8_t* id);
 int jr_comm_init(int rank, int world, const uint8_t* id, int device, jr_comm** comm);
-int jr_comm_init_file(int rank, int world, const char* uid_path, int device, int timeout_ms, jr_comm** comm);
+int jr_comm_init_file(int rank, int world, const char* uid_path, const char* run_id, int device, int timeout_ms,
+                      jr_comm** comm);
 /* buf[0..n) = sum over the ranks of buf[0..n), dtype JR_F32 or JR_BF16 */
 int jr_allreduce_sum(jr_comm* comm, void* buf, size_t n, int dtype, void* stream);
 int jr_comm_rank(const jr_comm* comm);

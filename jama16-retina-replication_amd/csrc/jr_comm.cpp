@@ -10,7 +10,8 @@
 // caller's stream, so it can run on a dedicated comm stream beside the
 // backward kernels and be captured in a HIP graph.  The unique id is either
 // passed in (exchanged by the caller's own bootstrap) or handed over through
-// a file (rank 0 writes it with an atomic rename, the others poll for it).
+// a file tagged with the caller's run id (rank 0 writes it with an atomic
+// rename, the others poll for the file of their run).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -19,6 +20,8 @@
 #include <cstring>
 #include <string>
 #include <thread>
+
+#include <unistd.h>
 
 #include "jr_common.h"
 
@@ -62,31 +65,53 @@ JR_API int jr_comm_init(int rank, int world, const uint8_t* id, int device, jr_c
   return JR_OK;
 }
 
-JR_API int jr_comm_init_file(int rank, int world, const char* uid_path, int device, int timeout_ms, jr_comm** out) {
-  if (!uid_path || !out) return fail(JR_ERR_INVALID, "comm_init_file: bad arguments");
+// The id file holds a magic, the caller's run id and the 128-byte id.  Rank
+// 0 publishes it with an atomic rename; every other rank polls until a file
+// with ITS run id appears, so an id left at uid_path by an earlier job (a
+// different run id) is never joined (that rank would have
+// waited in ncclCommInitRank on a communicator that no longer exists).
+static const char kUidMagic[8] = {'J', 'R', 'C', 'O', 'M', 'M', 'I', 'D'};
+
+JR_API int jr_comm_init_file(int rank, int world, const char* uid_path, const char* run_id, int device, int timeout_ms,
+                             jr_comm** out) {
+  if (!uid_path || !out || !run_id || !run_id[0]) return fail(JR_ERR_INVALID, "comm_init_file: bad arguments (uid_path, non-empty run_id)");
+  const std::string path(uid_path), run(run_id);
+  if (run.size() > 4096) return fail(JR_ERR_INVALID, "comm_init_file: run_id longer than 4096 bytes");
   uint8_t id[NCCL_UNIQUE_ID_BYTES];
-  const std::string path(uid_path);
   if (rank == 0) {
     int rc = jr_comm_unique_id(id);
     if (rc) return rc;
-    const std::string tmp = path + ".tmp";
+    const std::string tmp = path + ".tmp." + std::to_string((long long)getpid());
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) return fail(JR_ERR_INVALID, "comm_init_file: cannot write " + tmp);
-    const size_t w = std::fwrite(id, 1, sizeof(id), f);
-    std::fclose(f);
-    if (w != sizeof(id) || std::rename(tmp.c_str(), path.c_str()) != 0)
+    const uint32_t n = (uint32_t)run.size();
+    bool ok = std::fwrite(kUidMagic, 1, sizeof(kUidMagic), f) == sizeof(kUidMagic);
+    ok = ok && std::fwrite(&n, 1, sizeof(n), f) == sizeof(n);
+    ok = ok && std::fwrite(run.data(), 1, n, f) == n;
+    ok = ok && std::fwrite(id, 1, sizeof(id), f) == sizeof(id);
+    ok = std::fclose(f) == 0 && ok;
+    if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0)
       return fail(JR_ERR_INVALID, "comm_init_file: cannot publish " + path);
   } else {
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
       FILE* f = std::fopen(path.c_str(), "rb");
       if (f) {
-        const size_t n = std::fread(id, 1, sizeof(id), f);
+        char magic[sizeof(kUidMagic)];
+        uint32_t n = 0;
+        bool ok = std::fread(magic, 1, sizeof(magic), f) == sizeof(magic) &&
+                  std::memcmp(magic, kUidMagic, sizeof(magic)) == 0 && std::fread(&n, 1, sizeof(n), f) == sizeof(n) &&
+                  n == run.size();
+        if (ok) {
+          std::string got(n, '\0');
+          ok = std::fread(&got[0], 1, n, f) == n && got == run && std::fread(id, 1, sizeof(id), f) == sizeof(id);
+        }
         std::fclose(f);
-        if (n == sizeof(id)) break;
+        if (ok) break;   // else: absent, partial, foreign or stale -- keep polling
       }
       const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0);
-      if (timeout_ms >= 0 && ms.count() > timeout_ms) return fail(JR_ERR_INVALID, "comm_init_file: timed out waiting for " + path);
+      if (timeout_ms >= 0 && ms.count() > timeout_ms)
+        return fail(JR_ERR_INVALID, "comm_init_file: timed out waiting for " + path + " of run " + run);
       std::this_thread::sleep_for(std::chrono::milliseconds(10));
     }
   }

@@ -627,13 +627,25 @@ static int std_count(int dtype) {
 // filter-gradient GEMMs, whose per-wave split VALU outweighs the 8-product
 // MFMA gain, the fp32 MFMA is the faster one -- autotuning and the pinned
 // tables choose per GEMM (the planner heuristic keeps x8).
-static int cfg_count(int dtype) {
-  return std_count(dtype) + (dtype == JR_BF16 ? kNumHaloBf16 : dtype == JR_F32_X8 ? kNumCfgs : 0);
+// JR_BF16 ids: [0, 17) GEMM tiles, [17, 25) halo configs, then the wide
+// (8-wave) tiles; JR_F32_X8P: [0, 17) tiles, then the wide ones (new ids are
+// appended so committed tile tables keep their meaning).
+static int wide_base(int dtype) {
+  return dtype == JR_BF16 ? kNumCfgsBf16 + kNumHaloBf16 : dtype == JR_F32_X8P ? kNumCfgsX8P : 1 << 20;
 }
-static bool is_halo(int dtype, int tile) { return dtype == JR_BF16 && tile >= kNumCfgsBf16; }
+static int cfg_count(int dtype) {
+  return dtype == JR_BF16 ? wide_base(dtype) + kNumCfgsBf16W
+         : dtype == JR_F32_X8P ? wide_base(dtype) + kNumCfgsX8PW
+         : std_count(dtype) + (dtype == JR_F32_X8 ? kNumCfgs : 0);
+}
+static bool is_halo(int dtype, int tile) {
+  return dtype == JR_BF16 && tile >= kNumCfgsBf16 && tile < kNumCfgsBf16 + kNumHaloBf16;
+}
+static bool is_wide(int dtype, int tile) { return tile >= wide_base(dtype) && tile < cfg_count(dtype); }
 static bool is_x8_f32(int dtype, int tile) { return dtype == JR_F32_X8 && tile >= kNumCfgs; }
 static const TileCfg& tile_cfg(int dtype, int tile) {
   if (is_halo(dtype, tile)) return kHaloBf16[tile - kNumCfgsBf16].t;
+  if (is_wide(dtype, tile)) return (dtype == JR_BF16 ? kCfgsBf16W : kCfgsX8PW)[tile - wide_base(dtype)];
   if (is_x8_f32(dtype, tile)) return kCfgs[tile - kNumCfgs];
   return (dtype == JR_BF16 ? kCfgsBf16 : dtype == JR_F32_X8P ? kCfgsX8P : kCfgs)[tile];
 }
@@ -705,6 +717,19 @@ static int heuristic_cfg(int dtype, int M, int N, int K) {
 typedef std::array<int, 13> TuneKey;
 static std::mutex g_tune_mu;
 static std::map<TuneKey, int> g_tuned;
+// bumped whenever an entry of g_tuned changes value (set_config, autotune):
+// a caller that bound plans (split-K slab sizes) to the overrides it applied
+// re-applies them when the generation moved (jr_conv2d_config_generation)
+static unsigned long long g_tune_gen = 1;
+static void tune_set(const TuneKey& k, int cfg) {   // g_tune_mu held; cfg < 0 erases
+  auto it = g_tuned.find(k);
+  if (cfg < 0) {
+    if (it != g_tuned.end()) { g_tuned.erase(it); ++g_tune_gen; }
+  } else if (it == g_tuned.end() || it->second != cfg) {
+    g_tuned[k] = cfg;
+    ++g_tune_gen;
+  }
+}
 
 static TuneKey tune_key(int dtype, int op, int M, int N, int K, const jr_conv_desc* d) {
   return TuneKey{dtype, op, M, N, K, d->h, d->w, d->kh, d->kw, d->stride_h, d->c_in, d->c_out, d->n};
@@ -849,6 +874,16 @@ static void fill_common(ConvArgs& a, const jr_conv_desc* d, int dtype) {
   a.xo = d->x_c_off; a.xs = d->x_c_stride; a.yo = d->y_c_off; a.ys = d->y_c_stride;
 }
 
+#ifdef JR_STAMPS
+static unsigned long long* g_dbg_stamps = nullptr;
+// diagnostic builds: every following conv GEMM launch writes 8 stamps per
+// block into p (ConvArgs::dbg; the caller sizes it for the grid)
+JR_API int jr_debug_set_stamps(void* p) {
+  g_dbg_stamps = static_cast<unsigned long long*>(p);
+  return JR_OK;
+}
+#endif
+
 // One GEMM (plus its split-K reduce) on the stream.
 // defer (WGRAD): write the split-K slabs into ws and stop (jr_wgrad_reduce
 // sums them later, batched with other layers').
@@ -865,6 +900,7 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     a.stats_p = sP;
   }
   a.M = p.M; a.N = p.N; a.K = p.K;
+  JR_ST(a.dbg = g_dbg_stamps;)
   a.ktiles = p.ktiles;
   a.kt_per_split = p.kt_per_split;
   a.ntn = p.nt;
@@ -884,7 +920,10 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
   } else if (bf16_operands(dtype)) {
     const TileCfg& t = tile_cfg(dtype, p.tile);
     const bool fast = OP == OP_WGRAD ? a.wo >= t.bk : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
-    launch_conv_bf16(OP, p.tile, fast, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
+    if (is_wide(dtype, p.tile))
+      launch_conv_bf16_wide(OP, p.tile - wide_base(dtype), fast, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
+    else
+      launch_conv_bf16(OP, p.tile, fast, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
   } else if (is_x8_f32(dtype, p.tile)) {
     launch_op<OP>(p.tile - kNumCfgs, a, grid, s);     // the fp32-MFMA kernel of that tile
   } else if (dtype == JR_F32_X8) {
@@ -1104,7 +1143,7 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
     }
     if (rc) break;
     std::lock_guard<std::mutex> lk(g_tune_mu);
-    g_tuned[tune_key(dtype, op, M, N, K, d)] = best_c;
+    tune_set(tune_key(dtype, op, M, N, K, d), best_c);
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
@@ -1252,7 +1291,13 @@ JR_API int jr_conv2d_bwd_filter_slabs(const jr_conv_desc* d, int dtype, const vo
     return fail(JR_ERR_INVALID, "bwd_filter_slabs: tensors must be 16-byte aligned");
   const Plan p = plan_for(d, OP_WGRAD, dtype, nullptr);
   if (p.splits <= 1) return fail(JR_ERR_INVALID, "bwd_filter_slabs: the plan has no split-K (use jr_conv2d_bwd_filter)");
-  if (slab_bytes < plan_ws(p)) return fail(JR_ERR_WORKSPACE, "bwd_filter_slabs: slab buffer too small for the plan");
+  // the slab region was sized by jr_conv2d_wgrad_seg for the split count the
+  // deferred reduce will sum: a plan that changed since (another caller's
+  // set_config / autotune on the same geometry) would leave stale slabs in
+  // that sum, so any mismatch fails loudly
+  if (slab_bytes != plan_ws(p))
+    return fail(JR_ERR_INVALID, "bwd_filter_slabs: the plan's split-K slab bytes differ from the segment's "
+                                "(tile configuration changed since jr_conv2d_wgrad_seg); re-bind the segment");
   ConvArgs a{};
   fill_common(a, d, dtype);
   a.A = static_cast<const float*>(x);
@@ -1368,11 +1413,13 @@ JR_API int jr_conv2d_set_config(const jr_conv_desc* d, int op, int dtype, int ph
   int M, N, K;
   gemm_dims(d, op, dtype, op == OP_DGRAD ? &ph[phase] : nullptr, &M, &N, &K);
   std::lock_guard<std::mutex> lk(g_tune_mu);
-  if (cfg < 0)
-    g_tuned.erase(tune_key(dtype, op, M, N, K, d));   // back to the planner's choice
-  else
-    g_tuned[tune_key(dtype, op, M, N, K, d)] = cfg;
+  tune_set(tune_key(dtype, op, M, N, K, d), cfg);   // cfg < 0: back to the planner's choice
   return JR_OK;
+}
+
+JR_API unsigned long long jr_conv2d_config_generation(void) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  return g_tune_gen;
 }
 
 JR_API int jr_conv2d_get_config(const jr_conv_desc* d, int op, int dtype, int phase) {

@@ -39,10 +39,11 @@ __device__ __forceinline__ s16x4 lds_tr(const uint16_t* p) {
       (__attribute__((address_space(3))) s16x4*)(const_cast<uint16_t*>(p)));
 }
 
-template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, int NP>
-__global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, int NP, int NW>
+__global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
   static_assert(NP == 1 || NP == 3, "one bf16 plane, or the h / m / l planes of X8P");
-  constexpr int WGN = 4 / WGM;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves per block");
+  constexpr int WGN = NW / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
   static_assert(WM % 32 == 0 && WN % 32 == 0, "wave tile must be a multiple of 32x32");
@@ -53,13 +54,15 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   constexpr bool MC = (OP == OP_WGRAD);       // both operands MC (else both KC)
   constexpr int ASZ = BM * BK, BSZ = BN * BK;  // bf16 elements per image
   constexpr int A_INSTR = ASZ / 512, B_INSTR = BSZ / 512;
-  constexpr int A_PW = (A_INSTR + 3) / 4, B_PW = (B_INSTR + 3) / 4;  // per wave
+  constexpr int A_PW = (A_INSTR + NW - 1) / NW, B_PW = (B_INSTR + NW - 1) / NW;  // per wave
   static_assert(ASZ % 512 == 0 && BSZ % 512 == 0, "tile must be whole DMA instructions");
   static_assert(BK % 16 == 0 && QPR <= 8, "BK must be 16..64");
   constexpr int STAGE = NP * (ASZ + BSZ);    // one ring slot: NP A planes, then NP B planes
-  constexpr int SMEM = NBUF * STAGE > 8 * stage_floats<WN>() ? NBUF * STAGE : 8 * stage_floats<WN>();
+  constexpr int SMEM = NBUF * STAGE > 2 * NW * stage_floats<WN>() ? NBUF * STAGE : 2 * NW * stage_floats<WN>();
+  static_assert(SMEM * 2 <= 160 * 1024, "LDS budget of one CU");
   __shared__ __attribute__((aligned(1024))) uint16_t smem[SMEM];
 
+  JR_ST(Stamps stamp; stamp.start();)
   const uint16_t* __restrict__ gA = reinterpret_cast<const uint16_t*>(g.A);
   const uint16_t* __restrict__ gB = reinterpret_cast<const uint16_t*>(g.B);
   const int tid = threadIdx.x;
@@ -85,11 +88,11 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   int a_s0[A_PW], a_s1[A_PW], a_s2[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
-    const int j = wave + 4 * i;
+    const int j = wave + NW * i;
     a_ptr[i] = zp;
     a_p0[i] = a_p1[i] = a_p2[i] = 0;
     a_s0[i] = a_s1[i] = a_s2[i] = 0;
-    if (A_INSTR % 4 != 0 && j >= A_INSTR) continue;
+    if (A_INSTR % NW != 0 && j >= A_INSTR) continue;
     if constexpr (!MC) {
       const int row = j * RPI + lane / QPR;
       const int q = (lane % QPR) ^ ((row / SWZ) % QPR);
@@ -158,10 +161,10 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   int b_p0[B_PW], b_s0[B_PW], b_s1[B_PW], b_s2[B_PW];
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
-    const int j = wave + 4 * i;
+    const int j = wave + NW * i;
     b_ptr[i] = zp;
     b_p0[i] = b_s0[i] = b_s1[i] = b_s2[i] = 0;
-    if (B_INSTR % 4 != 0 && j >= B_INSTR) continue;
+    if (B_INSTR % NW != 0 && j >= B_INSTR) continue;
     if constexpr (!MC) {
       const int row = j * RPI + lane / QPR;
       const int q = (lane % QPR) ^ ((row / SWZ) % QPR);
@@ -207,8 +210,8 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   auto issue_piece = [&](int kt, int d, uint16_t* __restrict__ As, uint16_t* __restrict__ Bs) {
     if (d < A_PW) {
       const int i = d;
-      const int j = wave + 4 * i;
-      if (A_INSTR % 4 != 0 && j >= A_INSTR) return;
+      const int j = wave + NW * i;
+      if (A_INSTR % NW != 0 && j >= A_INSTR) return;
       if constexpr (!MC && ut) {
         long long off;
         int dr, dc;
@@ -246,8 +249,8 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
       return;
     }
     const int i = d - A_PW;
-    const int j = wave + 4 * i;
-    if (B_INSTR % 4 != 0 && j >= B_INSTR) return;
+    const int j = wave + NW * i;
+    if (B_INSTR % NW != 0 && j >= B_INSTR) return;
     if constexpr (OP == OP_FWD) {
       const int k = b_s0[i] + (kt - kt0) * BK;
       const bool ok = b_p0[i] >= 0 && k < g.K;
@@ -298,7 +301,7 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
   const int l31 = lane & 31, lh = lane >> 5;
   // transposed-read lane roles (MC): 16-lane group g16 = lh*2 + hb
   const int hb = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
-  constexpr int per_tile = NP * (A_INSTR / 4 + B_INSTR / 4);   // DMA instructions per wave and tile (min)
+  constexpr int per_tile = NP * (A_INSTR / NW + B_INSTR / NW);   // DMA instructions per wave and tile (min)
 
   auto step = [&](int kt, auto do_issue, const uint16_t* __restrict__ As, const uint16_t* __restrict__ Bs,
                   uint16_t* __restrict__ wA, uint16_t* __restrict__ wB) {
@@ -382,75 +385,102 @@ __global__ void __launch_bounds__(256) k_conv_bf16(ConvArgs g) {
       if (kt0 + p < kt1) issue(kt0 + p, buf_a(p), buf_b(p));
     wait_vmcnt(per_tile * min(NBUF - 2, kt1 - kt0 - 1));
     __builtin_amdgcn_s_barrier();
+    JR_ST(stamp.prologue();)
     int cur = 0;
     int kt = kt0;
     for (; kt < kt1 - (NBUF - 1); ++kt) {
       const int nxt = cur == 0 ? NBUF - 1 : cur - 1;
       step(kt, std::true_type{}, buf_a(cur), buf_b(cur), buf_a(nxt), buf_b(nxt));
       __builtin_amdgcn_sched_barrier(0);
+      JR_ST(const unsigned long long tw = stamp.now();)
       wait_vmcnt(per_tile * (NBUF - 2));
       __builtin_amdgcn_s_barrier();
+      JR_ST(stamp.w += stamp.now() - tw;)
       __builtin_amdgcn_sched_barrier(0);
       cur = cur + 1 == NBUF ? 0 : cur + 1;
     }
     for (; kt < kt1; ++kt) {
       step(kt, std::false_type{}, buf_a(cur), buf_b(cur), nullptr, nullptr);
       __builtin_amdgcn_sched_barrier(0);
+      JR_ST(const unsigned long long tw = stamp.now();)
       wait_vmcnt(per_tile * max(0, min(NBUF - 2, kt1 - kt - 2)));
       __builtin_amdgcn_s_barrier();
+      JR_ST(stamp.w += stamp.now() - tw;)
       __builtin_amdgcn_sched_barrier(0);
       cur = cur + 1 == NBUF ? 0 : cur + 1;
     }
   }
+  JR_ST(stamp.loop();)
 
   // ---------------------------------------------------------------- epilogue
   conv_epilogue<OP, WM, TM, TN, NP == 1>(g, acc, reinterpret_cast<float*>(smem) + wave * stage_floats<WN>(), m0 + wm0,
                                       n0 + wn0, lane);
+  JR_ST(stamp.end(g.dbg);)
 }
 
-template <int OP, int C, int NP>
-static void launch_tile(bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  constexpr TileCfg t = NP == 1 ? kCfgsBf16[C] : kCfgsX8P[C];
+template <int OP, int NP, int BM, int BN, int WGM, int BK, int NBUF, int NW>
+static void launch_cfg_t(bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
   if (fast)
-    hipLaunchKernelGGL((k_conv_bf16<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, NP>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, true, NP, NW>), grid, dim3(64 * NW), 0, s, a);
   else
-    hipLaunchKernelGGL((k_conv_bf16<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, NP>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, false, NP, NW>), grid, dim3(64 * NW), 0, s, a);
 }
 
-template <int OP, int NP>
-static void launch_op_bf16(int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  static_assert(kNumCfgsBf16 == 17 && kNumCfgsX8P == 17, "keep the switch in sync with kCfgsBf16 / kCfgsX8P");
-  switch (tile) {
-    case 0: launch_tile<OP, 0, NP>(fast, a, grid, s); break;
-    case 1: launch_tile<OP, 1, NP>(fast, a, grid, s); break;
-    case 2: launch_tile<OP, 2, NP>(fast, a, grid, s); break;
-    case 3: launch_tile<OP, 3, NP>(fast, a, grid, s); break;
-    case 4: launch_tile<OP, 4, NP>(fast, a, grid, s); break;
-    case 5: launch_tile<OP, 5, NP>(fast, a, grid, s); break;
-    case 6: launch_tile<OP, 6, NP>(fast, a, grid, s); break;
-    case 7: launch_tile<OP, 7, NP>(fast, a, grid, s); break;
-    case 8: launch_tile<OP, 8, NP>(fast, a, grid, s); break;
-    case 9: launch_tile<OP, 9, NP>(fast, a, grid, s); break;
-    case 10: launch_tile<OP, 10, NP>(fast, a, grid, s); break;
-    case 11: launch_tile<OP, 11, NP>(fast, a, grid, s); break;
-    case 12: launch_tile<OP, 12, NP>(fast, a, grid, s); break;
-    case 13: launch_tile<OP, 13, NP>(fast, a, grid, s); break;
-    case 14: launch_tile<OP, 14, NP>(fast, a, grid, s); break;
-    case 15: launch_tile<OP, 15, NP>(fast, a, grid, s); break;
-    default: launch_tile<OP, 16, NP>(fast, a, grid, s); break;
+// config c of the standard (W = false) or wide (W = true) table of NP
+template <int OP, int C, int NP, bool W>
+static void launch_tile(bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
+  if constexpr (W) {
+    constexpr int n = NP == 1 ? kNumCfgsBf16W : kNumCfgsX8PW;
+    if constexpr (C < n) {
+      constexpr TileCfg t = NP == 1 ? kCfgsBf16W[C] : kCfgsX8PW[C];
+      launch_cfg_t<OP, NP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, t.nw>(fast, a, grid, s);
+    }
+  } else {
+    constexpr TileCfg t = NP == 1 ? kCfgsBf16[C] : kCfgsX8P[C];
+    launch_cfg_t<OP, NP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, t.nw>(fast, a, grid, s);
   }
 }
 
-template <int NP>
+template <int OP, int NP, bool W>
+static void launch_op_bf16(int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
+  static_assert(kNumCfgsBf16 == 17 && kNumCfgsX8P == 17, "keep the switch in sync with kCfgsBf16 / kCfgsX8P");
+  static_assert(kNumCfgsBf16W <= 17 && kNumCfgsX8PW <= 17, "keep the switch in sync with the wide tables");
+  switch (tile) {
+    case 0: launch_tile<OP, 0, NP, W>(fast, a, grid, s); break;
+    case 1: launch_tile<OP, 1, NP, W>(fast, a, grid, s); break;
+    case 2: launch_tile<OP, 2, NP, W>(fast, a, grid, s); break;
+    case 3: launch_tile<OP, 3, NP, W>(fast, a, grid, s); break;
+    case 4: launch_tile<OP, 4, NP, W>(fast, a, grid, s); break;
+    case 5: launch_tile<OP, 5, NP, W>(fast, a, grid, s); break;
+    case 6: launch_tile<OP, 6, NP, W>(fast, a, grid, s); break;
+    case 7: launch_tile<OP, 7, NP, W>(fast, a, grid, s); break;
+    case 8: launch_tile<OP, 8, NP, W>(fast, a, grid, s); break;
+    case 9: launch_tile<OP, 9, NP, W>(fast, a, grid, s); break;
+    case 10: launch_tile<OP, 10, NP, W>(fast, a, grid, s); break;
+    case 11: launch_tile<OP, 11, NP, W>(fast, a, grid, s); break;
+    case 12: launch_tile<OP, 12, NP, W>(fast, a, grid, s); break;
+    case 13: launch_tile<OP, 13, NP, W>(fast, a, grid, s); break;
+    case 14: launch_tile<OP, 14, NP, W>(fast, a, grid, s); break;
+    case 15: launch_tile<OP, 15, NP, W>(fast, a, grid, s); break;
+    default: launch_tile<OP, 16, NP, W>(fast, a, grid, s); break;
+  }
+}
+
+template <int NP, bool W>
 static void launch_np(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  if (op == OP_FWD) launch_op_bf16<OP_FWD, NP>(tile, fast, a, grid, s);
-  else if (op == OP_DGRAD) launch_op_bf16<OP_DGRAD, NP>(tile, fast, a, grid, s);
-  else launch_op_bf16<OP_WGRAD, NP>(tile, fast, a, grid, s);
+  if (op == OP_FWD) launch_op_bf16<OP_FWD, NP, W>(tile, fast, a, grid, s);
+  else if (op == OP_DGRAD) launch_op_bf16<OP_DGRAD, NP, W>(tile, fast, a, grid, s);
+  else launch_op_bf16<OP_WGRAD, NP, W>(tile, fast, a, grid, s);
 }
 
 void launch_conv_bf16(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s, int np) {
-  if (np == 3) launch_np<3>(op, tile, fast, a, grid, s);
-  else launch_np<1>(op, tile, fast, a, grid, s);
+  if (np == 3) launch_np<3, false>(op, tile, fast, a, grid, s);
+  else launch_np<1, false>(op, tile, fast, a, grid, s);
+}
+
+void launch_conv_bf16_wide(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s, int np) {
+  if (np == 3) launch_np<3, true>(op, tile, fast, a, grid, s);
+  else launch_np<1, true>(op, tile, fast, a, grid, s);
 }
 
 }  // namespace jr

@@ -38,7 +38,39 @@ struct ConvArgs {
   long long a_ps, b_ps;
   // halo-tiled FWD (jr_conv_halo.hip): halo rows per block and slot columns
   int halo_nr, halo_wp;
+  // diagnostic builds only (-DJR_STAMPS, `make stamps`): per-block s_memtime /
+  // s_memrealtime stamps, 8 per block (jr_debug_set_stamps); nullptr otherwise
+  unsigned long long* dbg;
 };
+
+#ifdef JR_STAMPS
+// [0] realtime at start, [1] realtime at end (100 MHz), [2] cycles of the
+// prologue (ring fill to the first barrier), [3] cycles of the K loop, [4]
+// cycles of the epilogue, [5] cycles the loop spent in vmcnt waits +
+// barriers, [6] HW_ID, [7] XCC_ID -- of wave 0 of the block
+struct Stamps {
+  unsigned long long r0, c0, cp, cl, w;
+  __device__ __forceinline__ void start() {
+    r0 = __builtin_amdgcn_s_memrealtime();
+    c0 = __builtin_amdgcn_s_memtime();
+    w = 0;
+  }
+  __device__ __forceinline__ void prologue() { cp = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void loop() { cl = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ unsigned long long now() { return __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void end(unsigned long long* dbg) {
+    const unsigned long long ce = __builtin_amdgcn_s_memtime(), re = __builtin_amdgcn_s_memrealtime();
+    if (dbg == nullptr || threadIdx.x != 0) return;
+    unsigned long long* o = dbg + 8ull * (blockIdx.z * gridDim.x + blockIdx.x);
+    o[0] = r0; o[1] = re; o[2] = cp - c0; o[3] = cl - cp; o[4] = ce - cl; o[5] = w;
+    o[6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    o[7] = __builtin_amdgcn_s_getreg((3 << 11) | 20);    // HW_REG_XCC_ID
+  }
+};
+#define JR_ST(x) x
+#else
+#define JR_ST(x)
+#endif
 
 // Input pixel (over all images) of DGRAD row m of the phase.
 __device__ __forceinline__ long long dgrad_pix(const ConvArgs& g, int m) {
@@ -425,6 +457,7 @@ __global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict_
 struct TileCfg {
   int bm, bn, wgm, bk, nbuf;
   double eff;  // relative MFMA efficiency guess used to rank padded work
+  int nw = 4;  // waves per block (256 or 512 threads)
 };
 
 // Candidate tiles (block BMxBN, WGM waves along M, K-tile BK).  The planner
@@ -504,6 +537,37 @@ static constexpr TileCfg kCfgsX8P[] = {
 };
 constexpr int kNumCfgsX8P = sizeof(kCfgsX8P) / sizeof(kCfgsX8P[0]);
 
+// Wide tiles (round 3): 8 waves (512 threads, two per SIMD) on 256-row
+// blocks, one block per CU.  Per K-tile a block moves (BM + BN) * BK operand
+// elements through L2 -> LDS-DMA for BM * BN * BK MACs: at 128 x 128 that
+// ratio needs ~2x the L2 -> LDS rate a CU sustains (~70 GB/s: the bf16 GEMMs
+// ran at 0.1-0.2 of the MFMA peak and x8p at 0.57 MFMA busy), at 256 x 256
+// half of it.  Two waves per SIMD hide each other's DMA issue, LDS reads and
+// barrier waits.  Selectable config ids FOLLOW every older id (bf16: after
+// the halo configs; x8p: after kCfgsX8P), so the committed tile tables keep
+// their meaning.
+static constexpr TileCfg kCfgsBf16W[] = {
+    {256, 256, 2, 32, 3, 1.20, 8},   // 0: wave 128x64, 96 KiB
+    {256, 192, 4, 32, 3, 1.16, 8},   // 1: wave 64x96, 84 KiB
+    {256, 128, 4, 64, 2, 1.12, 8},   // 2: wave 64x64, 96 KiB
+    {128, 256, 2, 64, 2, 1.12, 8},   // 3: wave 64x64, 96 KiB
+    {256, 256, 2, 64, 2, 1.20, 8},   // 4: wave 128x64, 128 KiB
+    {256, 192, 4, 64, 2, 1.16, 8},   // 5: wave 64x96, 112 KiB
+    {256, 96, 8, 64, 2, 1.00, 8},    // 6: wave 32x96, 88 KiB
+    {256, 64, 8, 64, 3, 0.95, 8},    // 7: wave 32x64, 120 KiB
+};
+constexpr int kNumCfgsBf16W = sizeof(kCfgsBf16W) / sizeof(kCfgsBf16W[0]);
+static constexpr TileCfg kCfgsX8PW[] = {
+    {256, 256, 2, 16, 3, 1.20, 8},   // 0: wave 128x64, 144 KiB
+    {256, 192, 4, 16, 3, 1.16, 8},   // 1: wave 64x96, 126 KiB
+    {256, 128, 4, 16, 3, 1.12, 8},   // 2: wave 64x64, 108 KiB
+    {128, 256, 2, 16, 3, 1.12, 8},   // 3: wave 64x64, 108 KiB
+    {256, 96, 8, 16, 4, 1.00, 8},    // 4: wave 32x96, 132 KiB
+    {256, 64, 8, 16, 4, 0.95, 8},    // 5: wave 32x64, 120 KiB
+    {128, 192, 4, 16, 3, 1.05, 8},   // 6: wave 32x96, 90 KiB
+};
+constexpr int kNumCfgsX8PW = sizeof(kCfgsX8PW) / sizeof(kCfgsX8PW[0]);
+
 // Halo-tiled bf16 FWD configurations (jr_conv_halo.hip), bf16 tile ids
 // kNumCfgsBf16 + i: for stride-1 'same' convs of exactly this kh x kw with
 // c_in % 32 == 0 whose halo (output rows a BM tile spans + kh - 1) x (w + kw -
@@ -531,5 +595,7 @@ void launch_conv_halo(int h, const ConvArgs& a, dim3 grid, hipStream_t s);
 // (np = 1, JR_BF16) or kCfgsX8P (np = 3, JR_F32_X8P), fast = the
 // uniform-tap / single-carry kernel variant.
 void launch_conv_bf16(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s, int np = 1);
+// the same kernel on a wide tile: index into kCfgsBf16W (np = 1) / kCfgsX8PW (np = 3)
+void launch_conv_bf16_wide(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s, int np = 1);
 
 }  // namespace jr

@@ -119,6 +119,14 @@ void up_h2v2_row(const uint8_t* __restrict near, const uint8_t* __restrict far, 
   }
 }
 
+// jdsample.c h1v2_fancy_upsample (libjpeg-turbo; 4:4:0 files, e.g. losslessly
+// transposed 4:2:2): out[c] = (3 near[c] + far[c] + bias) >> 2, bias 1 for the
+// upper output row of a pair (far = the row above), 2 for the lower one
+void up_v2_row(const uint8_t* __restrict near, const uint8_t* __restrict far, int w, int bias,
+               uint8_t* __restrict out) {
+  for (int c = 0; c < w; ++c) out[c] = (uint8_t)((near[c] * 3 + far[c] + bias) >> 2);
+}
+
 }  // namespace
 
 JR_JPEG_API const char* jr_jpeg_last_error(void) { return g_err.c_str(); }
@@ -147,16 +155,21 @@ JR_JPEG_API int jr_jpeg_header(const uint8_t* data, size_t len, int32_t* height,
   return 0;
 }
 
-JR_JPEG_API int jr_jpeg_decode(const uint8_t* data, size_t len, uint8_t* out, int32_t height, int32_t width,
-                               int32_t channels, int32_t dct_method) {
-  if (!data || !out || height <= 0 || width <= 0 || (channels != 1 && channels != 3)) {
-    g_err = "jr_jpeg_decode: bad arguments";
-    return -1;
-  }
-  if (dct_method != JR_JPEG_IFAST && dct_method != JR_JPEG_ISLOW) {
-    g_err = "jr_jpeg_decode: dct_method must be JR_JPEG_IFAST or JR_JPEG_ISLOW";
-    return -1;
-  }
+namespace {
+
+// Every buffer of one decode.  It lives in jr_jpeg_decode's frame, OUTSIDE
+// the function that calls setjmp: libjpeg reports errors by longjmp, which
+// must not jump over the construction of objects with destructors (C++
+// [csetjmp]); decode_into only resizes these through a reference.
+struct DecodeBufs {
+  std::vector<uint8_t> plane[3];
+  std::vector<JSAMPROW> ptrs[3];
+  std::vector<uint8_t> up_cb, up_cr, tmp;
+  std::vector<int16_t> colsum;
+};
+
+int decode_into(DecodeBufs& bufs, const uint8_t* data, size_t len, uint8_t* out, int32_t height, int32_t width,
+                int32_t channels, int32_t dct_method) {
   jpeg_decompress_struct cinfo;
   ErrMgr err;
   cinfo.err = jpeg_std_error(&err.pub);
@@ -178,13 +191,15 @@ JR_JPEG_API int jr_jpeg_decode(const uint8_t* data, size_t len, uint8_t* out, in
     jpeg_destroy_decompress(&cinfo);
     return -1;
   }
-  // the turbo-equivalent output path: YCbCr (or grayscale) files whose chroma
-  // is full, h2v1 or h2v2 subsampled
+  // the turbo-equivalent output path: YCbCr files whose chroma is full
+  // (h1v1), h2v1, h1v2 (4:4:0) or h2v2 subsampled; anything else (4:1:1,
+  // ...) takes libjpeg 9's own output path below
   bool own = cinfo.jpeg_color_space == JCS_YCbCr && cinfo.num_components == 3;
   if (own) {
     const jpeg_component_info* cp = cinfo.comp_info;
     const int H = cinfo.max_h_samp_factor, V = cinfo.max_v_samp_factor;
-    own = cp[0].h_samp_factor == H && cp[0].v_samp_factor == V && (H == 1 || H == 2) && (V == 1 || V == 2);
+    own = cp[0].h_samp_factor == H && cp[0].v_samp_factor == V &&
+          (H == 1 || H == 2) && (V == 1 || V == 2);
     for (int k = 1; k < 3 && own; ++k) own = cp[k].h_samp_factor == 1 && cp[k].v_samp_factor == 1;
   }
   if (own) {
@@ -197,11 +212,11 @@ JR_JPEG_API int jr_jpeg_decode(const uint8_t* data, size_t len, uint8_t* out, in
     const int ch = (int)cinfo.comp_info[1].height_in_blocks * DCTSIZE;
     const int rows_per_call = V * DCTSIZE;
     // whole planes at component resolution (+ one iMCU row of slack)
-    std::vector<uint8_t> plane[3];
+    std::vector<uint8_t>* plane = bufs.plane;
     plane[0].resize((size_t)(lh + rows_per_call) * lw);
     plane[1].resize((size_t)(ch + DCTSIZE) * cw);
     plane[2].resize((size_t)(ch + DCTSIZE) * cw);
-    std::vector<JSAMPROW> ptrs[3];
+    std::vector<JSAMPROW>* ptrs = bufs.ptrs;
     ptrs[0].resize(rows_per_call);
     ptrs[1].resize(DCTSIZE);
     ptrs[2].resize(DCTSIZE);
@@ -217,8 +232,14 @@ JR_JPEG_API int jr_jpeg_decode(const uint8_t* data, size_t len, uint8_t* out, in
     }
     // downsampled (valid) chroma geometry, as jdmaster.c computes it
     const int dw = (width * 1 + H - 1) / H, dh = (height * 1 + V - 1) / V;
-    std::vector<uint8_t> up_cb((size_t)2 * dw + 2), up_cr((size_t)2 * dw + 2), tmp((size_t)3 * width);
-    std::vector<int16_t> colsum((size_t)dw + 2);
+    std::vector<uint8_t>& up_cb = bufs.up_cb;
+    std::vector<uint8_t>& up_cr = bufs.up_cr;
+    std::vector<uint8_t>& tmp = bufs.tmp;
+    std::vector<int16_t>& colsum = bufs.colsum;
+    up_cb.resize((size_t)2 * dw + 2);
+    up_cr.resize((size_t)2 * dw + 2);
+    tmp.resize((size_t)3 * width);
+    colsum.resize((size_t)dw + 2);
     for (int y = 0; y < height; ++y) {
       const uint8_t* Y = plane[0].data() + (size_t)y * lw;
       const uint8_t *cb, *cr;
@@ -230,7 +251,15 @@ JR_JPEG_API int jr_jpeg_decode(const uint8_t* data, size_t len, uint8_t* out, in
         up_h2(plane[2].data() + (size_t)y * cw, dw, up_cr.data());
         cb = up_cb.data();
         cr = up_cr.data();
-      } else {               // h2v2 (H == 2): row pair of chroma row cy
+      } else if (H == 1) {   // h1v2 (4:4:0): vertical triangle filter only
+        const int cy = y >> 1;
+        const int far = (y & 1) ? std::min(cy + 1, dh - 1) : std::max(cy - 1, 0);   // replicated edge rows
+        for (int k = 1; k < 3; ++k)
+          up_v2_row(plane[k].data() + (size_t)cy * cw, plane[k].data() + (size_t)far * cw, dw, (y & 1) ? 2 : 1,
+                    (k == 1 ? up_cb : up_cr).data());
+        cb = up_cb.data();
+        cr = up_cr.data();
+      } else {               // h2v2: row pair of chroma row cy
         const int cy = y >> 1;
         const int far = (y & 1) ? std::min(cy + 1, dh - 1) : std::max(cy - 1, 0);   // replicated edge rows
         for (int k = 1; k < 3; ++k) {
@@ -266,4 +295,20 @@ JR_JPEG_API int jr_jpeg_decode(const uint8_t* data, size_t len, uint8_t* out, in
   jpeg_finish_decompress(&cinfo);
   jpeg_destroy_decompress(&cinfo);
   return 0;
+}
+
+}  // namespace
+
+JR_JPEG_API int jr_jpeg_decode(const uint8_t* data, size_t len, uint8_t* out, int32_t height, int32_t width,
+                               int32_t channels, int32_t dct_method) {
+  if (!data || !out || height <= 0 || width <= 0 || (channels != 1 && channels != 3)) {
+    g_err = "jr_jpeg_decode: bad arguments";
+    return -1;
+  }
+  if (dct_method != JR_JPEG_IFAST && dct_method != JR_JPEG_ISLOW) {
+    g_err = "jr_jpeg_decode: dct_method must be JR_JPEG_IFAST or JR_JPEG_ISLOW";
+    return -1;
+  }
+  DecodeBufs bufs;
+  return decode_into(bufs, data, len, out, height, width, channels, dct_method);
 }

@@ -169,12 +169,22 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for the N > 1 path on a one-GPU box (as bench.py's):
+    # JR_ONE_DEVICE=1 puts every rank on cuda:0, JR_DIST_BACKEND=gloo replaces
+    # RCCL (which refuses two ranks on one device); the only collective here
+    # is the final all_gather_object of the predictions
+    if os.environ.get("JR_ONE_DEVICE") == "1" or os.environ.get("JR_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("JR_DIST_BACKEND", "nccl")
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     print(f"Numpy version: {np.__version__}")
     print(f"Torch version: {torch.__version__} (libjr / MI355X backend)")

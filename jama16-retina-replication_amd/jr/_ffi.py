@@ -83,6 +83,7 @@ _SIGS = {
                                    c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_get_config": (c_int, [POINTER(ConvDesc), c_int, c_int, c_int]),
     "jr_conv2d_set_config": (c_int, [POINTER(ConvDesc), c_int, c_int, c_int, c_int]),
+    "jr_conv2d_config_generation": (ctypes.c_ulonglong, []),
     "jr_conv2d_num_configs": (c_int, [c_int]),
     "jr_conv_weights_bf16_tiles": (c_int32, [c_int32, c_int32, c_int32, c_int32]),
     "jr_conv_weights_bf16": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p,
@@ -97,7 +98,7 @@ _SIGS = {
                              c_int64, c_void_p]),
     "jr_comm_unique_id": (c_int, [c_void_p]),
     "jr_comm_init": (c_int, [c_int, c_int, c_void_p, c_int, c_void_p]),
-    "jr_comm_init_file": (c_int, [c_int, c_int, c_char_p, c_int, c_int, c_void_p]),
+    "jr_comm_init_file": (c_int, [c_int, c_int, c_char_p, c_char_p, c_int, c_int, c_void_p]),
     "jr_allreduce_sum": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     "jr_comm_rank": (c_int, [c_void_p]),
     "jr_comm_world": (c_int, [c_void_p]),
@@ -157,6 +158,15 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    diag = os.environ.get("JR_LIB_DIAG")    # diagnostic builds only (e.g. libjr_stamps.so, `make stamps`)
+    if diag:
+        lib = ctypes.CDLL(diag)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libjr.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; "
@@ -210,7 +220,7 @@ def call(name: str, *args) -> int:
     lib = load()
     rc = getattr(lib, name)(*args)
     if isinstance(rc, int) and name not in ("jr_conv2d_workspace_size", "jr_bn_workspace_size",
-                                            "jr_conv2d_get_config", "jr_conv2d_num_configs",
+                                            "jr_conv2d_get_config", "jr_conv2d_num_configs", "jr_conv2d_config_generation",
                                             "jr_conv_weights_bf16_tiles"):
         check(name, rc)
     return rc

@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -66,12 +67,21 @@ class JrComm:
     """libjr's RCCL communicator (one per process / GPU)."""
 
     def __init__(self, rank: int, world: int, device: int, uid: Optional[bytes] = None,
-                 uid_path: Optional[str] = None, timeout_ms: int = 120000):
+                 uid_path: Optional[str] = None, timeout_ms: int = 120000, run_id: Optional[str] = None):
         self.lib = _ffi.load()
         self.h = ctypes.c_void_p()
         if uid_path is not None:
-            _ffi.check("jr_comm_init_file", self.lib.jr_comm_init_file(rank, world, uid_path.encode(), device,
-                                                                        timeout_ms, ctypes.byref(self.h)))
+            # the id file is tagged with the job's run id: a file an earlier job
+            # left at uid_path is ignored (default: the launcher's rendezvous id)
+            run_id = run_id or os.environ.get("TORCHELASTIC_RUN_ID") or (
+                f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}"
+                if "MASTER_ADDR" in os.environ and "MASTER_PORT" in os.environ else None)
+            if not run_id:
+                raise ValueError("JrComm(uid_path=...) needs a run_id shared by every rank of the job "
+                                 "(or TORCHELASTIC_RUN_ID / MASTER_ADDR+MASTER_PORT in the environment)")
+            _ffi.check("jr_comm_init_file", self.lib.jr_comm_init_file(rank, world, uid_path.encode(),
+                                                                        run_id.encode(), device, timeout_ms,
+                                                                        ctypes.byref(self.h)))
         else:
             if uid is None or len(uid) != 128:
                 raise ValueError("JrComm needs the 128-byte unique id of rank 0 (JrComm.unique_id())")

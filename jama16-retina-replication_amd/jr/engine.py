@@ -144,6 +144,7 @@ class Engine:
             if t is not None and all(u.name in t["configs"] for u in self.cunits):
                 self.set_tile_table(t)
                 self.tiles = "pinned"
+        self._own_tiles()
 
     # ------------------------------------------------------------------ memory
     def _t(self, n: int, dtype=torch.float32) -> torch.Tensor:
@@ -314,6 +315,7 @@ class Engine:
         self.synchronize()
         if self.train_mode:
             self.grads.zero_()
+        self._own_tiles()
 
     def conv_configs(self) -> dict:
         """{conv launch name: (fwd cfg, wgrad cfg, [dgrad cfg per phase])} in use."""
@@ -356,7 +358,29 @@ class Engine:
         if (table.get("conv_math"), table.get("batch"), table.get("height"), table.get("width")) != \
                 (self.conv_math, self.batch, self.g.height, self.g.width):
             raise ValueError("tile table is for another conv math / batch / resolution")
-        cfgs = table["configs"]
+        self._apply_configs(table["configs"])
+        self._own_tiles()
+
+    def _own_tiles(self) -> None:
+        """Record the configs this engine's call lists are bound to (libjr's
+        overrides are process-wide: another engine or caller of the same
+        geometry may change them; _ensure_tiles puts these back)."""
+        if not hasattr(self, "tiles"):
+            return                  # still in __init__ (clear_tile_table before the table is chosen)
+        self._tile_cfgs = self.tile_table()["configs"]
+        self._tile_gen = self.lib.jr_conv2d_config_generation()
+
+    def _ensure_tiles(self) -> None:
+        """Re-apply this engine's configs if libjr's overrides changed since it
+        applied them (the deferred filter-gradient segments bind
+        the split count of the plan at call-list build time)."""
+        gen = self.lib.jr_conv2d_config_generation()
+        if getattr(self, "_tile_cfgs", None) is None or gen == self._tile_gen:
+            return
+        self._apply_configs(self._tile_cfgs)     # the same plans the call lists were built with
+        self._tile_gen = self.lib.jr_conv2d_config_generation()
+
+    def _apply_configs(self, cfgs: dict) -> None:
         for u in self.cunits:
             f, wg, dg = cfgs[u.name]
             d = self._conv_desc(u, self.batch)
@@ -373,6 +397,10 @@ class Engine:
     def clear_tile_table(self) -> None:
         """Back to the deterministic planner heuristic for every conv launch
         (drops autotuned or pinned configs of this engine's geometries)."""
+        self._clear_configs()
+        self._own_tiles()
+
+    def _clear_configs(self) -> None:
         if hasattr(self, "_calls"):
             self._drop_calls()
         for u in self.cunits:
@@ -438,6 +466,7 @@ class Engine:
         (fwd, bwd, opt, keep, None).  one_stream: every call is bound to
         lane 0's stream (per-lane scratch kept) for the explicit-DAG graph
         capture, where the lanes become graph branches (capture())."""
+        self._ensure_tiles()
         nl = self.nlanes if nl is None else max(1, min(int(nl), self.nlanes))
         key = (B, nl, one_stream)
         if key in self._calls:

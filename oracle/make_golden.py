@@ -10,7 +10,7 @@ vectors (oracle/__init__.py).  These fixtures freeze the oracle's own outputs
 Weights are NOT stored: they are regenerated from the seed by jr.init
 (numpy PCG64), inputs from jr.synth (PCG64(432 + i)).
 
-  python oracle/make_golden.py [--only ops,metrics,net107,net299,curve,curve16,curve16bf,net299b64,net587b2]
+  python oracle/make_golden.py [--only ops,metrics,net107,net299,curve,curve16,curve16bf,net299b64,net587b2,eval299]
 
 BASELINE-size fixtures (net299b64: configs 2-3 geometry, 299^2 B=64;
 net587b2: config 5 geometry, 587^2 B=2) hold the fp64 results AND the same
@@ -144,6 +144,81 @@ def _net(res, batch, seed, steps=1, cycle=None, dtype="float64", proj=False, bf1
     return out
 
 
+EVAL299 = dict(n=280, res=299, batch=32, members=3, p=0.3, start=5000, label_seed=11)
+
+
+def eval_records(out_dir: str) -> None:
+    """The config-4 test set of the eval299b32 fixture: 280 synthetic fundus
+    images (299^2, JPEG q=100, labels Bernoulli(0.3)), ONE shard (the
+    reference lists shards in os.listdir order, lib/dataset.py:5-8, so one
+    shard keeps the record order fixed), as the GPU test rewrites it."""
+    from jr import synth_records
+    e = EVAL299
+    synth_records.write_split(out_dir, e["n"], e["res"], p=e["p"], start=e["start"], num_shards=1, name="test",
+                              label_seed=e["label_seed"])
+
+
+def eval_batches(data_dir: str, batch: int):
+    """(uint8 batches, label batches, sha256 of every decoded pixel) as
+    evaluate.predict_all reads them (lib.dataset, native decode, IFAST)."""
+    import hashlib
+    import lib.dataset as D
+    ds = D.initialize_dataset(data_dir, batch, num_workers=8, prefetch_buffer_size=2 * batch,
+                              image_data_format="channels_last", num_channels=3, image_dim=[299, 299],
+                              decode_dtype="uint8")
+    xs, ys, h = [], [], hashlib.sha256()
+    it = iter(ds)
+    try:
+        for x, y in it:
+            xs.append(np.array(x))
+            ys.append(np.array(y))
+            h.update(np.ascontiguousarray(xs[-1]).tobytes())
+    finally:
+        D.close_iterator(it)
+    return xs, ys, h.hexdigest()
+
+
+def eval299():
+    """BASELINE config 4 at its workload geometry:
+    evaluate.py -lm of 3 members (Keras init seeds 0-2) over 280 test images
+    at 299^2 in eval batches of 32 (the last one partial, 24), batch-statistics
+    BN per batch (App. C Q1).  fp64 oracle predictions per member, the linear
+    ensemble mean (evaluate.py:214-217) and its TF metrics (200-threshold AUC,
+    Brier, confusion and spec/sens at the 0.5 operating threshold)."""
+    import tempfile
+    import torch
+    from jr.inception import build_inception_v3
+    from jr.init import init_params, unflatten
+    from oracle.inception_ref import InceptionV3Ref
+    torch.set_num_threads(os.cpu_count() or 8)
+    e = EVAL299
+    with tempfile.TemporaryDirectory() as d:
+        eval_records(d)
+        xs, ys, digest = eval_batches(d, e["batch"])
+    g = build_inception_v3(e["res"], e["res"])
+    preds = []
+    for m in range(e["members"]):
+        ref = InceptionV3Ref(unflatten(g, init_params(g, m)), torch.float64, requires_grad=False)
+        pm = []
+        for x in xs:
+            with torch.no_grad():
+                _, p, _ = ref.forward(x.astype(np.float32) * np.float32(1 / 255))
+            pm.append(np.asarray(p, np.float64).reshape(-1, 1))
+        preds.append(np.vstack(pm))
+        print(f"eval299 member {m} done", flush=True)
+    preds = np.stack(preds)                           # [M, N, 1] fp64
+    labels = np.vstack(ys).astype(np.float32)
+    ens = preds.astype(np.float32).mean(axis=0)       # evaluate.py: np.mean of float32 predictions
+    thr = MR.generate_thresholds(200, 1e-7) + [0.5]
+    tp, fp, fn, tn = MR.counts_at_thresholds(labels, ens, thr)
+    spec, sens = MR.spec_sens(tp, fp, fn, tn)
+    np.savez_compressed(os.path.join(OUT, "eval_res299_b32.npz"), preds=preds, labels=labels, ens=ens,
+                        input_sha256=np.array(digest), auc=np.array(MR.auc(labels, ens)),
+                        brier=np.array(MR.brier(labels, ens)), confusion=MR.confusion_matrix(tp[-1], fp[-1], fn[-1],
+                                                                                             tn[-1]),
+                        spec=spec, sens=sens, **{k: np.array(v) for k, v in e.items()})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="ops,metrics,net107,net299,curve")
@@ -184,6 +259,9 @@ def main():
         curve["losses_bf16emu"] = _net(299, 16, 0, steps=100, cycle=32, bf16=True)["losses"]
         np.savez_compressed(p, **curve)
         print(f"curve16bf: {time.time() - t0:.0f}s", flush=True)
+    if "eval299" in todo:
+        eval299()
+        print(f"eval299: {time.time() - t0:.0f}s", flush=True)
     for key, res, batch in (("net299b64", 299, 64), ("net587b2", 587, 2)):
         if key in todo:
             d = _net(res, batch, 0, proj=True)

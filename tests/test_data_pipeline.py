@@ -330,6 +330,24 @@ def test_native_jpeg_decoder(records):
             assert np.abs(ifast - islow).max() <= 8
             fast_dev.append(np.abs(ifast - islow).ravel())
     assert np.concatenate(fast_dev).mean() < 1.0
+    # 4:4:0 (h1v2 chroma, e.g. a losslessly transposed 4:2:2 file): Pillow
+    # cannot write it, IJG's cjpeg (same image, /opt/conda) can; libjpeg-turbo's
+    # vertical-only triangle filter (the h2v2 path was taken and
+    # stretched the left half of the chroma row)
+    import shutil
+    import subprocess
+    cjpeg = shutil.which("cjpeg") or ("/opt/conda/bin/cjpeg" if os.path.exists("/opt/conda/bin/cjpeg") else None)
+    if cjpeg:
+        for h, w in ((61, 77), (64, 64), (1, 9), (2, 5)):
+            img = np.clip(rng.normal(120, 40, (h, w, 3)), 0, 255).astype(np.uint8)
+            ppm = b"P6\n%d %d\n255\n" % (w, h) + img.tobytes()
+            data = subprocess.run([cjpeg, "-quality", "95", "-sample", "1x2,1x1,1x1"], input=ppm,
+                                  capture_output=True, check=True).stdout
+            im = Image.open(io.BytesIO(data))
+            assert [s[1:3] for s in im.layer] == [(1, 2), (1, 1), (1, 1)]
+            pil = np.asarray(im.convert("RGB")).astype(int)
+            islow = J.decode(data, "islow").astype(int)
+            assert np.array_equal(islow, pil), (h, w, np.abs(islow - pil).max())
     gray = io.BytesIO()
     g = np.clip(rng.normal(120, 40, (61, 77)), 0, 255).astype(np.uint8)
     Image.fromarray(g).save(gray, "JPEG", quality=90)

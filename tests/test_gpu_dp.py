@@ -108,7 +108,7 @@ def test_jr_comm_rccl_world1(payload, tmp_path):
     from jr import _ffi
     from jr.dist import BucketAllReduce, JrComm
     from jr.engine import Engine
-    comm = JrComm(0, 1, 0, uid_path=str(tmp_path / "uid"))
+    comm = JrComm(0, 1, 0, uid_path=str(tmp_path / "uid"), run_id=f"test-{os.getpid()}")
     assert _ffi.load().jr_comm_world(comm.h) == 1
     x = torch.randn(1000, device="cuda")
     xb = x.to(torch.bfloat16)

@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 _KEEP = []
+WIDE_BF16 = 8          # jr_conv_impl.h kCfgsBf16W: the last config ids of JR_BF16
 
 
 @pytest.fixture(autouse=True)
@@ -80,7 +81,11 @@ def test_conv_fwd_bn_stats(case, dtype):
     wsb = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, dt) + 5 * n * ho * wo * cout * 4 + (1 << 20)
     ws = torch.zeros(wsb // 4 + 4, device="cuda")
     _KEEP.append(ws)
-    for cfg in (None, 0 | (1 << 8), 0 | (3 << 8), 3 | (1 << 8), 3 | (5 << 8), -1):
+    cfgs = [None, 0 | (1 << 8), 0 | (3 << 8), 3 | (1 << 8), 3 | (5 << 8)]
+    if dtype == "bf16":     # the wide 8-wave tiles (ids after the halo configs): epilogue and split-K statistics
+        wide0 = L.jr_conv2d_num_configs(1) - WIDE_BF16
+        cfgs += [wide0 | (1 << 8), (wide0 + 1) | (1 << 8), (wide0 + 6) | (1 << 8), (wide0 + 2) | (3 << 8)]
+    for cfg in cfgs + [-1]:
         if cfg is not None:
             _ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, dt, 0, cfg))
         Y = torch.zeros(n * ho * wo * cout, dtype=tdt, device="cuda")
