@@ -138,6 +138,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   static_assert(ASZ % 256 == 0 && BSZ % 256 == 0, "tile must be whole DMA instructions");
   constexpr int SMEM = NBUF * (ASZ + BSZ) > 4 * stage_floats<WN>() ? NBUF * (ASZ + BSZ) : 4 * stage_floats<WN>();
   __shared__ __attribute__((aligned(1024))) float smem[SMEM];
+  JR_ST(Stamps stamp; stamp.start();)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -153,19 +154,31 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   const float* zp = g_zero_page;
   const int cred = OP == OP_FWD ? g.cp : g.cout;       // channel radix of the KC k index
   // FWD/DGRAD: UT = wave-uniform tap (host guarantees cred % BK == 0).
-  // WGRAD: UT = single-carry pixel counters (host guarantees wo >= BK).
+  // WGRAD: UT = incremental pixel walk (host guarantees BK / wo < ho: one
+  // carry per radix and K-tile), else the mixed-radix loop.
   constexpr bool ut = UT && OP != OP_WGRAD;
+  // WGRAD UT (round 3): every piece keeps its element offset a_off and adds
+  // one of three wave-uniform deltas per K-tile by its carries (no
+  // multiplies: the rebuilt address cost two v_mul_lo_u32 per piece and tile);
+  // single const definitions (assigned in branches they became allocas read
+  // through a per-lane select of their addresses)
+  const int wq = OP == OP_WGRAD ? BK / g.wo : 0, wr = OP == OP_WGRAD ? BK - wq * g.wo : 0;
+  const int dW0 = OP == OP_WGRAD ? (wq * g.sh * g.w + wr * g.sw) * g.xs : 0;
+  const int dW1 = OP == OP_WGRAD ? (g.sh * g.w - g.wo * g.sw) * g.xs : 0;
+  const int dW2 = OP == OP_WGRAD ? (g.h * g.w - g.ho * g.sh * g.w) * g.xs : 0;
 
   // ---------------------------------------------------------------- A state
   const float* a_ptr[A_PW];                 // per-slot base pointer (ut paths)
   int a_p0[A_PW], a_p1[A_PW], a_p2[A_PW];   // per-slot geometry fixed over K
   int a_s0[A_PW], a_s1[A_PW], a_s2[A_PW];   // per-lane k counters (generic / WGRAD)
+  int a_off[A_PW];                          // WGRAD UT: element offset from a_ptr
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     const int j = wave + 4 * i;
     a_ptr[i] = zp;
     a_p0[i] = a_p1[i] = a_p2[i] = 0;
     a_s0[i] = a_s1[i] = a_s2[i] = 0;
+    a_off[i] = 0;
     if (A_INSTR % 4 != 0 && j >= A_INSTR) continue;
     if constexpr (A_KC) {
       const int row = j * RPI + lane / QPR;
@@ -228,6 +241,8 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       const int rem = pix - a_s0[i] * hw;
       a_s1[i] = rem / g.wo;                     // oh
       a_s2[i] = rem - a_s1[i] * g.wo;           // ow
+      if (m < g.M) a_ptr[i] = g.A + ((long long)(a_p0[i] * g.w + a_p1[i]) * g.xs + g.xo + a_p2[i]);
+      a_off[i] = ((a_s0[i] * g.h + a_s1[i] * g.sh) * g.w + a_s2[i] * g.sw) * g.xs;
     }
   }
   // ---------------------------------------------------------------- B state
@@ -308,6 +323,20 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
           const float* p = g.A + ((a_p2[i] + oh * g.wo + ow) * g.ys + g.yo + a_s2[i]);
           src = ok ? p : zp;
           adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cout, g.nb, a_multi);
+        } else if constexpr (UT) {  // WGRAD, incremental: (image, oh, ow) += BK pixels
+          const int hi = __mul24(a_s1[i], g.sh) + a_p0[i], wi = __mul24(a_s2[i], g.sw) + a_p1[i];
+          const bool ok = (a_s0[i] < g.n) & ((unsigned)hi < (unsigned)g.h) & ((unsigned)wi < (unsigned)g.w);
+          src = ok ? a_ptr[i] + a_off[i] : zp;
+          int ow = a_s2[i] + wr;
+          const bool c1 = ow >= g.wo;
+          ow -= c1 ? g.wo : 0;
+          int oh = a_s1[i] + wq + (c1 ? 1 : 0);
+          const bool c2 = oh >= g.ho;
+          oh -= c2 ? g.ho : 0;
+          a_off[i] += dW0 + (c1 ? dW1 : 0) + (c2 ? dW2 : 0);
+          a_s2[i] = ow;
+          a_s1[i] = oh;
+          a_s0[i] += c2 ? 1 : 0;
         } else {  // WGRAD
           const int hi = a_s1[i] * g.sh + a_p0[i], wi = a_s2[i] * g.sw + a_p1[i];
           const bool ok = a_s0[i] < g.n && (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w;
@@ -559,6 +588,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       if (kt0 + p < kt1) issue(kt0 + p, smem + p * (ASZ + BSZ), smem + p * (ASZ + BSZ) + ASZ);
     wait_vmcnt(per_tile * min(NBUF - 2, kt1 - kt0 - 1));
     __builtin_amdgcn_s_barrier();
+    JR_ST(stamp.prologue();)
     int cur = 0;
     int kt = kt0;
     // steady state: NBUF-1 tiles in flight after this iteration's issue;
@@ -571,8 +601,10 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       // the wait; one barrier: every wave's part of tile kt+1 is in LDS and
       // every wave is done reading tile kt
       __builtin_amdgcn_sched_barrier(0);
+      JR_ST(const unsigned long long tw = stamp.now();)
       wait_vmcnt(per_tile * (NBUF - 2));
       __builtin_amdgcn_s_barrier();
+      JR_ST(stamp.w += stamp.now() - tw;)
       __builtin_amdgcn_sched_barrier(0);
       cur = cur + 1 == NBUF ? 0 : cur + 1;
     }
@@ -580,15 +612,19 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     for (; kt < kt1; ++kt) {
       step(kt, std::false_type{}, smem + cur * (ASZ + BSZ), smem + cur * (ASZ + BSZ) + ASZ, nullptr, nullptr);
       __builtin_amdgcn_sched_barrier(0);
+      JR_ST(const unsigned long long tw = stamp.now();)
       wait_vmcnt(per_tile * max(0, min(NBUF - 2, kt1 - kt - 2)));
       __builtin_amdgcn_s_barrier();
+      JR_ST(stamp.w += stamp.now() - tw;)
       __builtin_amdgcn_sched_barrier(0);
       cur = cur + 1 == NBUF ? 0 : cur + 1;
     }
   }
+  JR_ST(stamp.loop();)
 
   // ---------------------------------------------------------------- epilogue
   conv_epilogue<OP, WM, TM, TN, false>(g, acc, smem + wave * stage_floats<WN>(), m0 + wm0, n0 + wn0, lane);
+  JR_ST(stamp.end(g.dbg);)
 }
 
 // ---------------------------------------------------------------- host side
@@ -799,11 +835,12 @@ static size_t stats_ws(int dtype, const Plan& p) {
 }
 
 // Fast-path kernels (UT): FWD/DGRAD when the reduction channel radix is a
-// multiple of BK (every layer but conv1 FWD at BK = 16); WGRAD when wo >= BK.
+// multiple of BK (every layer but conv1 FWD at BK = 16); WGRAD when BK / wo < ho
+// (one carry per radix and K-tile: the incremental pixel walk).
 template <int OP, int C, int DBG, bool X8>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t s) {
   constexpr TileCfg t = kCfgs[C];
-  const bool fast = OP == OP_WGRAD ? a.wo >= t.bk : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
+  const bool fast = OP == OP_WGRAD ? t.bk / a.wo < a.ho : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
   if (fast) {
     hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, X8, DBG>), grid, dim3(256), 0, s, a);
     return;
@@ -918,12 +955,23 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     a.halo_nr = (h.t.bm + a.wo - 2) / a.wo + 1 + a.kh - 1;
     launch_conv_halo(p.tile - kNumCfgsBf16, a, grid, s);
   } else if (bf16_operands(dtype)) {
+    // operand address mode (k_conv_bf16 AM): the tap is wave-uniform when the
+    // reduction channel radix is a multiple of BK (0), else every piece walks
+    // its own address with at most one carry per radix and K-tile (1), else
+    // the mixed-radix loop (2: conv1's 8 channels; WGRAD on images shorter
+    // than BK / wo rows)
     const TileCfg& t = tile_cfg(dtype, p.tile);
-    const bool fast = OP == OP_WGRAD ? a.wo >= t.bk : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
+    int am;
+    if (OP == OP_WGRAD) {
+      am = t.bk / a.wo < a.ho ? 1 : 2;
+    } else {
+      const int cred = OP == OP_FWD ? a.cp : a.cout;
+      am = cred % t.bk == 0 ? 0 : cred >= t.bk ? 1 : 2;
+    }
     if (is_wide(dtype, p.tile))
-      launch_conv_bf16_wide(OP, p.tile - wide_base(dtype), fast, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
+      launch_conv_bf16_wide(OP, p.tile - wide_base(dtype), am, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
     else
-      launch_conv_bf16(OP, p.tile, fast, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
+      launch_conv_bf16(OP, p.tile, am, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
   } else if (is_x8_f32(dtype, p.tile)) {
     launch_op<OP>(p.tile - kNumCfgs, a, grid, s);     // the fp32-MFMA kernel of that tile
   } else if (dtype == JR_F32_X8) {

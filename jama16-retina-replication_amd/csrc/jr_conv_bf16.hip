@@ -39,7 +39,11 @@ __device__ __forceinline__ s16x4 lds_tr(const uint16_t* p) {
       (__attribute__((address_space(3))) s16x4*)(const_cast<uint16_t*>(p)));
 }
 
-template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, int NP, int NW>
+// AM = operand address mode (host: run_gemm): 0 = wave-uniform tap (FWD /
+// DGRAD with cred % BK == 0), 1 = incremental per-lane walk (one carry per
+// radix per K-tile), 2 = mixed-radix loop (conv1's 8 padded channels, tiny
+// images).
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, int AM, int NP, int NW>
 __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
   static_assert(NP == 1 || NP == 3, "one bf16 plane, or the h / m / l planes of X8P");
   static_assert(NW == 4 || NW == 8, "4 or 8 waves per block");
@@ -76,22 +80,48 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
   const int m0 = mt * BM, n0 = nt * BN;
   const int kt0 = blockIdx.z * g.kt_per_split;
   const int kt1 = min(g.ktiles, kt0 + g.kt_per_split);
-  const uint16_t* zp = reinterpret_cast<const uint16_t*>(g_zero_page);
+  // the zero page's address lives in an SGPR pair for the whole kernel (hipcc
+  // otherwise rematerialises it with s_getpc + two v_mov per DMA piece)
+  unsigned long long zpa = reinterpret_cast<unsigned long long>(g_zero_page);
+  asm volatile("" : "+s"(zpa));
+  const uint16_t* zp = reinterpret_cast<const uint16_t*>(zpa);
   const int cred = OP == OP_FWD ? g.cp : g.cout;
   const long long psA = NP > 1 ? g.a_ps : 0, psB = NP > 1 ? g.b_ps : 0;
-  // FWD/DGRAD: UT = wave-uniform tap (cred % BK == 0); WGRAD: UT = wo >= BK.
-  constexpr bool ut = UT && OP != OP_WGRAD;
+  constexpr bool ut = AM == 0 && OP != OP_WGRAD;
 
   // ---------------------------------------------------------------- A state
+  // AM 1: pieces walk their im2col address INCREMENTALLY (round 3): a_ptr =
+  // the piece's base, a_off = the element offset of its current k, advanced
+  // per K-tile by one of three wave-uniform deltas chosen by the piece's
+  // carries -- no multiplies, no division (the mixed-radix form rebuilt the
+  // address with two v_mul_lo_u32 and ~35 more VALU per piece and tile:
+  // conv5's loop issued 19 VALU per MFMA).  Needs at most one carry per
+  // radix per K-tile, which the host checks.
+  const int wq = OP == OP_WGRAD ? BK / g.wo : 0, wr = OP == OP_WGRAD ? BK - wq * g.wo : 0;
+  constexpr bool inc_a = AM == 1;
+  constexpr bool inc_b = OP == OP_DGRAD && AM == 1;
+  // (single const definitions: deltas assigned in branches became allocas
+  // that hipcc then read through a per-lane select of their ADDRESSES --
+  // scratch and flat loads in the K loop)
+  const int dA0 = OP == OP_WGRAD ? (wq * g.sh * g.w + wr * g.sw) * g.xs : BK;
+  const int dA1 = OP == OP_FWD ? BK - g.cp + g.xs
+                  : OP == OP_DGRAD ? BK - g.cout - g.ys
+                                   : (g.sh * g.w - g.wo * g.sw) * g.xs;
+  const int dA2 = OP == OP_FWD ? BK - g.cp + g.xs + (g.w - g.kw) * g.xs
+                  : OP == OP_DGRAD ? BK - g.cout + (g.nb - 1 - g.wo) * g.ys
+                                   : (g.h * g.w - g.ho * g.sh * g.w) * g.xs;
+  const int dB1 = OP == OP_DGRAD ? BK - g.cout + g.sw * g.cin * g.cout : 0;
+  const int dB2 = OP == OP_DGRAD ? BK - g.cout + (g.sh * g.kw - g.sw * (g.nb - 1)) * g.cin * g.cout : 0;
   const uint16_t* a_ptr[A_PW];
   int a_p0[A_PW], a_p1[A_PW], a_p2[A_PW];
-  int a_s0[A_PW], a_s1[A_PW], a_s2[A_PW];
+  int a_s0[A_PW], a_s1[A_PW], a_s2[A_PW], a_off[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     const int j = wave + NW * i;
     a_ptr[i] = zp;
     a_p0[i] = a_p1[i] = a_p2[i] = 0;
     a_s0[i] = a_s1[i] = a_s2[i] = 0;
+    a_off[i] = 0;
     if (A_INSTR % NW != 0 && j >= A_INSTR) continue;
     if constexpr (!MC) {
       const int row = j * RPI + lane / QPR;
@@ -111,11 +141,12 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
         } else {
           a_p0[i] = -(1 << 28);
         }
-        a_ptr[i] = gA + ((long long)pix * g.xs + g.xo + q * 8);
+        a_ptr[i] = gA + ((long long)pix * g.xs + g.xo + (ut ? q * 8 : 0));
         const int rc = k / g.cp;
         a_s2[i] = k - rc * g.cp;
         a_s0[i] = rc / g.kw;
         a_s1[i] = rc - a_s0[i] * g.kw;
+        a_off[i] = (a_s0[i] * g.w + a_s1[i]) * g.xs + a_s2[i];
       } else {  // DGRAD
         int pix = 0;
         if (m < g.M) {
@@ -129,11 +160,12 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
         } else {
           a_p0[i] = -(1 << 28);
         }
-        a_ptr[i] = gA + ((long long)pix * g.ys + g.yo + q * 8);
+        a_ptr[i] = gA + ((long long)pix * g.ys + g.yo + (ut ? q * 8 : 0));
         const int ab = k / g.cout;
         a_s2[i] = k - ab * g.cout;
         a_s0[i] = ab / g.nb;
         a_s1[i] = ab - a_s0[i] * g.nb;
+        a_off[i] = a_s2[i] - (a_s0[i] * g.wo + a_s1[i]) * g.ys;
       }
     } else {  // WGRAD MC: m = (r,c,ci) fixed per slot (8 channels), k = pixel
       const int flat = j * 512 + lane * 8;
@@ -154,16 +186,18 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
       const int rem = pix - a_s0[i] * hw;
       a_s1[i] = rem / g.wo;
       a_s2[i] = rem - a_s1[i] * g.wo;
+      if (m < g.M) a_ptr[i] = gA + ((long long)(a_p0[i] * g.w + a_p1[i]) * g.xs + g.xo + a_p2[i]);
+      a_off[i] = ((a_s0[i] * g.h + a_s1[i] * g.sh) * g.w + a_s2[i] * g.sw) * g.xs;
     }
   }
   // ---------------------------------------------------------------- B state
   const uint16_t* b_ptr[B_PW];
-  int b_p0[B_PW], b_s0[B_PW], b_s1[B_PW], b_s2[B_PW];
+  int b_p0[B_PW], b_s0[B_PW], b_s1[B_PW], b_s2[B_PW], b_off[B_PW];
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
     const int j = wave + NW * i;
     b_ptr[i] = zp;
-    b_p0[i] = b_s0[i] = b_s1[i] = b_s2[i] = 0;
+    b_p0[i] = b_s0[i] = b_s1[i] = b_s2[i] = b_off[i] = 0;
     if (B_INSTR % NW != 0 && j >= B_INSTR) continue;
     if constexpr (!MC) {
       const int row = j * RPI + lane / QPR;
@@ -175,11 +209,12 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
         b_s0[i] = k;
         b_ptr[i] = gB + ((long long)(nn < g.N ? nn : 0) * g.K + k);
       } else {                        // DGRAD: W[(r,c)][ci][co], rows = ci, k = (a, bb, co)
-        b_ptr[i] = gB + ((long long)(nn < g.N ? nn : 0) * g.cout + q * 8);
+        b_ptr[i] = gB + ((long long)(nn < g.N ? nn : 0) * g.cout + (ut ? q * 8 : 0));
         const int ab = k / g.cout;
         b_s2[i] = k - ab * g.cout;
         b_s0[i] = ab / g.nb;
         b_s1[i] = ab - b_s0[i] * g.nb;
+        b_off[i] = ((g.r0 + g.sh * b_s0[i]) * g.kw + g.c0 + g.sw * b_s1[i]) * g.cin * g.cout + b_s2[i];
       }
     } else {  // WGRAD MC: dy rows = k (pixels), cols = n
       const int flat = j * 512 + lane * 8;
@@ -198,16 +233,18 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
     t_c = rc - t_r * (OP == OP_FWD ? g.kw : g.nb);
   }
 
-  const bool a_multi = !MC ? (cred < BK) : (!UT && g.wo < BK);
-  const bool b_multi = (OP == OP_DGRAD) ? (g.cout < BK) : false;
+  constexpr bool a_multi = AM == 2;
+  constexpr bool b_multi = OP == OP_DGRAD && AM == 2;
 
+  // (every bounds test below combines with bitwise &: && made hipcc branch
+  // around each operand with exec-mask saves)
   // One piece into every plane image (out-of-bounds: the zero page, all planes).
-  auto put = [&](bool ok, const uint16_t* src, uint16_t* dst, long long ps, int isz) {
+  auto put = [&](bool ok, const uint16_t* src, uint16_t* dst, long long ps, int isz) __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) dma16(ok ? src + p * ps : zp, dst + p * isz);
   };
   // DMA of one operand piece of tile kt (d < A_PW: A slot d, else B slot).
-  auto issue_piece = [&](int kt, int d, uint16_t* __restrict__ As, uint16_t* __restrict__ Bs) {
+  auto issue_piece = [&](int kt, int d, uint16_t* __restrict__ As, uint16_t* __restrict__ Bs) __attribute__((always_inline)) {
     if (d < A_PW) {
       const int i = d;
       const int j = wave + NW * i;
@@ -223,26 +260,58 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
           dr = -t_r; dc = -t_c;
         }
         const int hmax = OP == OP_FWD ? g.h : g.ho, wmax = OP == OP_FWD ? g.w : g.wo;
-        const bool ok = (unsigned)(a_p0[i] + dr) < (unsigned)hmax && (unsigned)(a_p1[i] + dc) < (unsigned)wmax;
+        const bool ok = ((unsigned)(a_p0[i] + dr) < (unsigned)hmax) & ((unsigned)(a_p1[i] + dc) < (unsigned)wmax);
         put(ok, a_ptr[i] + off, As + j * 512, psA, ASZ);
       } else {
         bool ok;
         const uint16_t* p;
         if constexpr (OP == OP_FWD) {
           const int hi = a_p0[i] + a_s0[i], wi = a_p1[i] + a_s1[i];
-          ok = (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w && a_s0[i] < g.kh;
-          p = gA + ((a_p2[i] + hi * g.w + wi) * g.xs + g.xo + a_s2[i]);
-          adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cp, g.kw, a_multi);
+          ok = ((unsigned)hi < (unsigned)g.h) & ((unsigned)wi < (unsigned)g.w) & (a_s0[i] < g.kh);
+          if constexpr (inc_a) {   // (r, c, ch) += BK channels, one carry at most per radix
+            p = a_ptr[i] + a_off[i];
+            const bool c1 = a_s2[i] + BK >= g.cp, c2 = c1 & (a_s1[i] + 1 == g.kw);
+            a_off[i] += dA0 + (c1 ? dA1 - dA0 : 0) + (c2 ? dA2 - dA1 : 0);
+            a_s2[i] += c1 ? BK - g.cp : BK;
+            a_s1[i] = c2 ? 0 : a_s1[i] + (c1 ? 1 : 0);
+            a_s0[i] += c2 ? 1 : 0;
+          } else {
+            p = gA + ((a_p2[i] + hi * g.w + wi) * g.xs + g.xo + a_s2[i]);
+            adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cp, g.kw, a_multi);
+          }
         } else if constexpr (OP == OP_DGRAD) {
           const int oh = a_p0[i] - a_s0[i], ow = a_p1[i] - a_s1[i];
-          ok = (unsigned)oh < (unsigned)g.ho && (unsigned)ow < (unsigned)g.wo && a_s0[i] < g.na;
-          p = gA + ((a_p2[i] + oh * g.wo + ow) * g.ys + g.yo + a_s2[i]);
-          adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cout, g.nb, a_multi);
+          ok = ((unsigned)oh < (unsigned)g.ho) & ((unsigned)ow < (unsigned)g.wo) & (a_s0[i] < g.na);
+          if constexpr (inc_a) {   // (a, b, co) += BK output channels
+            p = a_ptr[i] + a_off[i];
+            const bool c1 = a_s2[i] + BK >= g.cout, c2 = c1 & (a_s1[i] + 1 == g.nb);
+            a_off[i] += dA0 + (c1 ? dA1 - dA0 : 0) + (c2 ? dA2 - dA1 : 0);
+            a_s2[i] += c1 ? BK - g.cout : BK;
+            a_s1[i] = c2 ? 0 : a_s1[i] + (c1 ? 1 : 0);
+            a_s0[i] += c2 ? 1 : 0;
+          } else {
+            p = gA + ((a_p2[i] + oh * g.wo + ow) * g.ys + g.yo + a_s2[i]);
+            adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.cout, g.nb, a_multi);
+          }
         } else {  // WGRAD
-          const int hi = a_s1[i] * g.sh + a_p0[i], wi = a_s2[i] * g.sw + a_p1[i];
-          ok = a_s0[i] < g.n && (unsigned)hi < (unsigned)g.h && (unsigned)wi < (unsigned)g.w;
-          p = gA + (((a_s0[i] * g.h + hi) * g.w + wi) * g.xs + g.xo + a_p2[i]);
-          adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.wo, g.ho, a_multi);
+          const int hi = __mul24(a_s1[i], g.sh) + a_p0[i], wi = __mul24(a_s2[i], g.sw) + a_p1[i];
+          ok = (a_s0[i] < g.n) & ((unsigned)hi < (unsigned)g.h) & ((unsigned)wi < (unsigned)g.w);
+          if constexpr (inc_a) {   // (image, oh, ow) += BK = wq rows + wr columns of output pixels
+            p = a_ptr[i] + a_off[i];
+            int ow = a_s2[i] + wr;
+            const bool c1 = ow >= g.wo;
+            ow -= c1 ? g.wo : 0;
+            int oh = a_s1[i] + wq + (c1 ? 1 : 0);
+            const bool c2 = oh >= g.ho;
+            oh -= c2 ? g.ho : 0;
+            a_off[i] += dA0 + (c1 ? dA1 : 0) + (c2 ? dA2 : 0);
+            a_s2[i] = ow;
+            a_s1[i] = oh;
+            a_s0[i] += c2 ? 1 : 0;
+          } else {
+            p = gA + (((a_s0[i] * g.h + hi) * g.w + wi) * g.xs + g.xo + a_p2[i]);
+            adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.wo, g.ho, a_multi);
+          }
         }
         put(ok, p, As + j * 512, psA, ASZ);
       }
@@ -253,26 +322,35 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
     if (B_INSTR % NW != 0 && j >= B_INSTR) return;
     if constexpr (OP == OP_FWD) {
       const int k = b_s0[i] + (kt - kt0) * BK;
-      const bool ok = b_p0[i] >= 0 && k < g.K;
+      const bool ok = (b_p0[i] >= 0) & (k < g.K);
       put(ok, b_ptr[i] + (kt - kt0) * BK, Bs + j * 512, psB, BSZ);
     } else if constexpr (OP == OP_DGRAD) {
       if constexpr (ut) {
         const long long off = (long long)((g.r0 + g.sh * t_r) * g.kw + (g.c0 + g.sw * t_c)) * g.cin * g.cout + t_ch;
         put(b_p0[i] >= 0, b_ptr[i] + off, Bs + j * 512, psB, BSZ);
       } else {
-        const bool ok = b_p0[i] >= 0 && b_s0[i] < g.na;
-        const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
-        const uint16_t* p = gB + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
-        put(ok, p, Bs + j * 512, psB, BSZ);
-        adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
+        const bool ok = (b_p0[i] >= 0) & (b_s0[i] < g.na);
+        if constexpr (inc_b) {   // (a, b, co) += BK, taps r = r0 + sh a, c = c0 + sw b
+          put(ok, b_ptr[i] + b_off[i], Bs + j * 512, psB, BSZ);
+          const bool c1 = b_s2[i] + BK >= g.cout, c2 = c1 & (b_s1[i] + 1 == g.nb);
+          b_off[i] += BK + (c1 ? dB1 - BK : 0) + (c2 ? dB2 - dB1 : 0);
+          b_s2[i] += c1 ? BK - g.cout : BK;
+          b_s1[i] = c2 ? 0 : b_s1[i] + (c1 ? 1 : 0);
+          b_s0[i] += c2 ? 1 : 0;
+        } else {
+          const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
+          const uint16_t* p = gB + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
+          put(ok, p, Bs + j * 512, psB, BSZ);
+          adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
+        }
       }
     } else {  // WGRAD
       const int k = b_s0[i] + (kt - kt0) * BK;
-      const bool ok = b_p0[i] >= 0 && k < g.K;
+      const bool ok = (b_p0[i] >= 0) & (k < g.K);
       put(ok, b_ptr[i] + (long long)(kt - kt0) * BK * g.ys, Bs + j * 512, psB, BSZ);
     }
   };
-  auto advance = [&]() {
+  auto advance = [&]() __attribute__((always_inline)) {
     if constexpr (ut) {
       t_ch += BK;
       const bool w1 = t_ch == cred;
@@ -284,7 +362,7 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
     }
   };
   constexpr int NPIECE = A_PW + B_PW;
-  auto issue = [&](int kt, uint16_t* __restrict__ As, uint16_t* __restrict__ Bs) {
+  auto issue = [&](int kt, uint16_t* __restrict__ As, uint16_t* __restrict__ Bs) __attribute__((always_inline)) {
 #pragma unroll
     for (int d = 0; d < NPIECE; ++d) issue_piece(kt, d, As, Bs);
     advance();
@@ -304,7 +382,7 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
   constexpr int per_tile = NP * (A_INSTR / NW + B_INSTR / NW);   // DMA instructions per wave and tile (min)
 
   auto step = [&](int kt, auto do_issue, const uint16_t* __restrict__ As, const uint16_t* __restrict__ Bs,
-                  uint16_t* __restrict__ wA, uint16_t* __restrict__ wB) {
+                  uint16_t* __restrict__ wA, uint16_t* __restrict__ wB) __attribute__((always_inline)) {
     constexpr bool DO_ISSUE = decltype(do_issue)::value;
     bf16x8 af[NP][TM][KSTEPS], bfr[NP][TN][KSTEPS];
 #pragma unroll
@@ -376,8 +454,8 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
     }
     if constexpr (DO_ISSUE) advance();
   };
-  auto buf_a = [&](int b) { return smem + b * STAGE; };
-  auto buf_b = [&](int b) { return smem + b * STAGE + NP * ASZ; };
+  auto buf_a = [&](int b) __attribute__((always_inline)) { return smem + b * STAGE; };
+  auto buf_b = [&](int b) __attribute__((always_inline)) { return smem + b * STAGE + NP * ASZ; };
 
   if (kt0 < kt1) {
 #pragma unroll
@@ -419,68 +497,74 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
 }
 
 template <int OP, int NP, int BM, int BN, int WGM, int BK, int NBUF, int NW>
-static void launch_cfg_t(bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  if (fast)
-    hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, true, NP, NW>), grid, dim3(64 * NW), 0, s, a);
+static void launch_cfg_t(int am, const ConvArgs& a, dim3 grid, hipStream_t s) {
+  if constexpr (OP != OP_WGRAD) {
+    if (am == 0) {
+      hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, 0, NP, NW>), grid, dim3(64 * NW), 0, s, a);
+      return;
+    }
+  }
+  if (am == 1)
+    hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, 1, NP, NW>), grid, dim3(64 * NW), 0, s, a);
   else
-    hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, false, NP, NW>), grid, dim3(64 * NW), 0, s, a);
+    hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, 2, NP, NW>), grid, dim3(64 * NW), 0, s, a);
 }
 
 // config c of the standard (W = false) or wide (W = true) table of NP
 template <int OP, int C, int NP, bool W>
-static void launch_tile(bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
+static void launch_tile(int am, const ConvArgs& a, dim3 grid, hipStream_t s) {
   if constexpr (W) {
     constexpr int n = NP == 1 ? kNumCfgsBf16W : kNumCfgsX8PW;
     if constexpr (C < n) {
       constexpr TileCfg t = NP == 1 ? kCfgsBf16W[C] : kCfgsX8PW[C];
-      launch_cfg_t<OP, NP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, t.nw>(fast, a, grid, s);
+      launch_cfg_t<OP, NP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, t.nw>(am, a, grid, s);
     }
   } else {
     constexpr TileCfg t = NP == 1 ? kCfgsBf16[C] : kCfgsX8P[C];
-    launch_cfg_t<OP, NP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, t.nw>(fast, a, grid, s);
+    launch_cfg_t<OP, NP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, t.nw>(am, a, grid, s);
   }
 }
 
 template <int OP, int NP, bool W>
-static void launch_op_bf16(int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
+static void launch_op_bf16(int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s) {
   static_assert(kNumCfgsBf16 == 17 && kNumCfgsX8P == 17, "keep the switch in sync with kCfgsBf16 / kCfgsX8P");
   static_assert(kNumCfgsBf16W <= 17 && kNumCfgsX8PW <= 17, "keep the switch in sync with the wide tables");
   switch (tile) {
-    case 0: launch_tile<OP, 0, NP, W>(fast, a, grid, s); break;
-    case 1: launch_tile<OP, 1, NP, W>(fast, a, grid, s); break;
-    case 2: launch_tile<OP, 2, NP, W>(fast, a, grid, s); break;
-    case 3: launch_tile<OP, 3, NP, W>(fast, a, grid, s); break;
-    case 4: launch_tile<OP, 4, NP, W>(fast, a, grid, s); break;
-    case 5: launch_tile<OP, 5, NP, W>(fast, a, grid, s); break;
-    case 6: launch_tile<OP, 6, NP, W>(fast, a, grid, s); break;
-    case 7: launch_tile<OP, 7, NP, W>(fast, a, grid, s); break;
-    case 8: launch_tile<OP, 8, NP, W>(fast, a, grid, s); break;
-    case 9: launch_tile<OP, 9, NP, W>(fast, a, grid, s); break;
-    case 10: launch_tile<OP, 10, NP, W>(fast, a, grid, s); break;
-    case 11: launch_tile<OP, 11, NP, W>(fast, a, grid, s); break;
-    case 12: launch_tile<OP, 12, NP, W>(fast, a, grid, s); break;
-    case 13: launch_tile<OP, 13, NP, W>(fast, a, grid, s); break;
-    case 14: launch_tile<OP, 14, NP, W>(fast, a, grid, s); break;
-    case 15: launch_tile<OP, 15, NP, W>(fast, a, grid, s); break;
-    default: launch_tile<OP, 16, NP, W>(fast, a, grid, s); break;
+    case 0: launch_tile<OP, 0, NP, W>(am, a, grid, s); break;
+    case 1: launch_tile<OP, 1, NP, W>(am, a, grid, s); break;
+    case 2: launch_tile<OP, 2, NP, W>(am, a, grid, s); break;
+    case 3: launch_tile<OP, 3, NP, W>(am, a, grid, s); break;
+    case 4: launch_tile<OP, 4, NP, W>(am, a, grid, s); break;
+    case 5: launch_tile<OP, 5, NP, W>(am, a, grid, s); break;
+    case 6: launch_tile<OP, 6, NP, W>(am, a, grid, s); break;
+    case 7: launch_tile<OP, 7, NP, W>(am, a, grid, s); break;
+    case 8: launch_tile<OP, 8, NP, W>(am, a, grid, s); break;
+    case 9: launch_tile<OP, 9, NP, W>(am, a, grid, s); break;
+    case 10: launch_tile<OP, 10, NP, W>(am, a, grid, s); break;
+    case 11: launch_tile<OP, 11, NP, W>(am, a, grid, s); break;
+    case 12: launch_tile<OP, 12, NP, W>(am, a, grid, s); break;
+    case 13: launch_tile<OP, 13, NP, W>(am, a, grid, s); break;
+    case 14: launch_tile<OP, 14, NP, W>(am, a, grid, s); break;
+    case 15: launch_tile<OP, 15, NP, W>(am, a, grid, s); break;
+    default: launch_tile<OP, 16, NP, W>(am, a, grid, s); break;
   }
 }
 
 template <int NP, bool W>
-static void launch_np(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  if (op == OP_FWD) launch_op_bf16<OP_FWD, NP, W>(tile, fast, a, grid, s);
-  else if (op == OP_DGRAD) launch_op_bf16<OP_DGRAD, NP, W>(tile, fast, a, grid, s);
-  else launch_op_bf16<OP_WGRAD, NP, W>(tile, fast, a, grid, s);
+static void launch_np(int op, int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s) {
+  if (op == OP_FWD) launch_op_bf16<OP_FWD, NP, W>(tile, am, a, grid, s);
+  else if (op == OP_DGRAD) launch_op_bf16<OP_DGRAD, NP, W>(tile, am, a, grid, s);
+  else launch_op_bf16<OP_WGRAD, NP, W>(tile, am, a, grid, s);
 }
 
-void launch_conv_bf16(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s, int np) {
-  if (np == 3) launch_np<3, false>(op, tile, fast, a, grid, s);
-  else launch_np<1, false>(op, tile, fast, a, grid, s);
+void launch_conv_bf16(int op, int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s, int np) {
+  if (np == 3) launch_np<3, false>(op, tile, am, a, grid, s);
+  else launch_np<1, false>(op, tile, am, a, grid, s);
 }
 
-void launch_conv_bf16_wide(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s, int np) {
-  if (np == 3) launch_np<3, true>(op, tile, fast, a, grid, s);
-  else launch_np<1, true>(op, tile, fast, a, grid, s);
+void launch_conv_bf16_wide(int op, int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s, int np) {
+  if (np == 3) launch_np<3, true>(op, tile, am, a, grid, s);
+  else launch_np<1, true>(op, tile, am, a, grid, s);
 }
 
 }  // namespace jr

@@ -592,10 +592,10 @@ constexpr int kNumHaloBf16 = sizeof(kHaloBf16) / sizeof(kHaloBf16[0]);
 void launch_conv_halo(int h, const ConvArgs& a, dim3 grid, hipStream_t s);
 
 // bf16-operand GEMM launch (jr_conv_bf16.hip): tile index into kCfgsBf16
-// (np = 1, JR_BF16) or kCfgsX8P (np = 3, JR_F32_X8P), fast = the
-// uniform-tap / single-carry kernel variant.
-void launch_conv_bf16(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s, int np = 1);
+// (np = 1, JR_BF16) or kCfgsX8P (np = 3, JR_F32_X8P).
+// am = operand address mode (k_conv_bf16's AM).
+void launch_conv_bf16(int op, int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s, int np = 1);
 // the same kernel on a wide tile: index into kCfgsBf16W (np = 1) / kCfgsX8PW (np = 3)
-void launch_conv_bf16_wide(int op, int tile, bool fast, const ConvArgs& a, dim3 grid, hipStream_t s, int np = 1);
+void launch_conv_bf16_wide(int op, int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s, int np = 1);
 
 }  // namespace jr

@@ -59,6 +59,8 @@ def build_parser():
                    help="path to where operating points metrics should be saved")
     p.add_argument("-b", "--batch_size", default=DEFAULT_BATCH_SIZE, help="batch size")
     p.add_argument("-op", "--operating_threshold", default=0.5, help="operating threshold")
+    p.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
+                   help="activation storage and conv arithmetic: f32 (the reference's; default) or bf16 MFMA")
     p.add_argument("--conv_math", default="x8", choices=["x8", "x8p", "f32"],
                    help="fp32 convolution arithmetic: x8 = exact 3-way bf16 split on the matrix cores (fp32-accurate, "
                         "default), x8p = the same on pre-split operand planes, f32 = fp32 MFMA")
@@ -79,7 +81,7 @@ def expand_model_paths(load_model_path: str):
     return [load_model_path]
 
 
-def make_engines(paths, meta, batch_size, device=0, conv_math="x8"):
+def make_engines(paths, meta, batch_size, device=0, conv_math="x8", dtype="f32"):
     """One inference engine per ensemble member, parameters loaded; conv
     tiles from the committed MI355X table of the eval workload (Engine
     tiles="pinned"; the heuristic where none matches): every member and every
@@ -89,7 +91,7 @@ def make_engines(paths, meta, batch_size, device=0, conv_math="x8"):
     engines = []
     for path in paths:
         eng = Engine(batch_size, meta["height"], meta["width"], meta.get("units", 1), device=device,
-                     train=False, conv_math=conv_math)
+                     train=False, dtype=dtype, conv_math=conv_math if dtype == "f32" else "bf16")
         flat, _ = checkpoint.load(path, eng.g)
         eng.load_params(flat)
         engines.append(eng)
@@ -186,10 +188,10 @@ def main(argv=None):
         else:
             dist.init_process_group(backend)
 
-    print(f"Numpy version: {np.__version__}")
-    print(f"Torch version: {torch.__version__} (libjr / MI355X backend)")
     random.seed(432)
-    if rank == 0:
+    if rank == 0:       # one copy of the reference's header lines, whatever the rank count
+        print(f"Numpy version: {np.__version__}")
+        print(f"Torch version: {torch.__version__} (libjr / MI355X backend)")
         print("""
 Evaluating: {},
 Saving operating thresholds metrics at: {},
@@ -199,7 +201,8 @@ Using operating treshold: {},
 
     thresholds = lib.metrics.generate_thresholds(NUM_THRESHOLDS, KEPSILON) + [operating_threshold]
     meta = checkpoint.read_meta(load_model_paths[0])
-    engines = make_engines(load_model_paths, meta, batch_size, device=local, conv_math=args.conv_math)
+    engines = make_engines(load_model_paths, meta, batch_size, device=local, conv_math=args.conv_math,
+                           dtype=args.dtype)
     preds, labels, order = predict_all(engines, data_dir, batch_size, rank, world)
 
     if dist:   # gather every rank's batches to rank 0, restore dataset order

@@ -94,8 +94,12 @@ class Engine:
         self.optimizer = optimizer
         self.lr = float(lr)
         self.momentum = float(momentum)
-        # Adam (north-star extra; TF AdamOptimizer defaults): accum holds m
+        # Adam (north-star extra; TF AdamOptimizer defaults): accum holds m;
+        # beta1_power / beta2_power are fp32 variables initialised to beta1 /
+        # beta2 and multiplied by them (fp32) after every step, as TF's
+        # AdamOptimizer._finish does
         self.adam_b1, self.adam_b2, self.adam_eps, self.adam_t = 0.9, 0.999, 1e-8, 0
+        self.adam_b1p, self.adam_b2p = np.float32(self.adam_b1), np.float32(self.adam_b2)
         self.head_mode = _ffi.JR_HEAD_SIGMOID if head == "sigmoid" else _ffi.JR_HEAD_SOFTMAX
         self.units = self.g.units
         # (diagnostic) JR_LANE_PRIORITY="p0,p1,...": HIP stream priority per lane
@@ -284,7 +288,7 @@ class Engine:
             return self.w_hwio.data_ptr() + 2 * self.wb_hwio_off[u.first.idx]
         return self.params.data_ptr() + 4 * u.koff
 
-    def autotune(self) -> None:
+    def autotune(self, progress: Optional[Callable[[str], None]] = None) -> None:
         """jr_conv2d_autotune every conv launch of the planned batch (cudnnFind
         style: times each tile configuration on this engine's own buffers and
         caches the fastest in libjr).  Runs before any data is loaded: it
@@ -297,6 +301,8 @@ class Engine:
             fn, args, name = self._wprep_call()
             _ffi.check(name, fn(*args))
         for u in self.cunits:
+            if progress is not None:
+                progress(u.name)
             d = self._conv_desc(u, B)
             x = (self.aplanes[u.x] if self.x8p else self.acts[u.x]).data_ptr()
             draw = (self.drawp_lane[0] if self.x8p else self.draw).data_ptr() if self.train_mode else 0
@@ -777,11 +783,17 @@ class Engine:
             args = list(c.args)
             args[-2] = grad_scale
             if self.optimizer == "adam":
-                # TF ApplyAdam's alpha = lr sqrt(1 - b2^t) / (1 - b1^t), host fp64
-                # (so Adam steps run eagerly: the scalar changes every step)
+                # TF ApplyAdam (training_ops.cc): alpha = lr * sqrt(1 - beta2_power)
+                # / (1 - beta1_power), evaluated in the variable dtype (fp32,
+                # left to right; np.sqrt of a float32 is correctly rounded like
+                # Eigen's), from fp32 beta powers (so Adam steps run eagerly:
+                # the scalar changes every step)
+                f = np.float32
                 self.adam_t += 1
-                t = self.adam_t
-                args[5] = self.lr * (1.0 - self.adam_b2 ** t) ** 0.5 / (1.0 - self.adam_b1 ** t)
+                alpha = f(f(self.lr) * np.sqrt(f(1) - self.adam_b2p)) / (f(1) - self.adam_b1p)
+                args[5] = float(f(alpha))
+                self.adam_b1p = f(self.adam_b1p * f(self.adam_b1))
+                self.adam_b2p = f(self.adam_b2p * f(self.adam_b2))
             opt = [dataclasses.replace(c, args=tuple(args))]
         self._run(opt, ev)
 

@@ -10,7 +10,7 @@ vectors (oracle/__init__.py).  These fixtures freeze the oracle's own outputs
 Weights are NOT stored: they are regenerated from the seed by jr.init
 (numpy PCG64), inputs from jr.synth (PCG64(432 + i)).
 
-  python oracle/make_golden.py [--only ops,metrics,net107,net299,curve,curve16,curve16bf,net299b64,net587b2,eval299]
+  python oracle/make_golden.py [--only ops,metrics,net107,net299,curve,curve16,curve16bf,net299b64,net587b2,eval299,curve16bf32]
 
 BASELINE-size fixtures (net299b64: configs 2-3 geometry, 299^2 B=64;
 net587b2: config 5 geometry, 587^2 B=2) hold the fp64 results AND the same
@@ -196,23 +196,32 @@ def eval299():
         eval_records(d)
         xs, ys, digest = eval_batches(d, e["batch"])
     g = build_inception_v3(e["res"], e["res"])
-    preds = []
+    preds, preds_bf = [], []
     for m in range(e["members"]):
-        ref = InceptionV3Ref(unflatten(g, init_params(g, m)), torch.float64, requires_grad=False)
-        pm = []
-        for x in xs:
-            with torch.no_grad():
-                _, p, _ = ref.forward(x.astype(np.float32) * np.float32(1 / 255))
-            pm.append(np.asarray(p, np.float64).reshape(-1, 1))
-        preds.append(np.vstack(pm))
+        for bf, out in ((False, preds), (True, preds_bf)):
+            # fp64, and the same forward with bf16 storage emulated where the
+            # GPU bf16 path stores bf16 (an independent bf16 implementation:
+            # its gap to fp64 is the envelope the bf16 engine is judged by)
+            ref = InceptionV3Ref(unflatten(g, init_params(g, m)), torch.float64, requires_grad=False,
+                                 emulate_bf16=bf)
+            pm = []
+            for x in xs:
+                with torch.no_grad():
+                    _, p, _ = ref.forward(x.astype(np.float32) * np.float32(1 / 255))
+                pm.append(np.asarray(p, np.float64).reshape(-1, 1))
+            out.append(np.vstack(pm))
         print(f"eval299 member {m} done", flush=True)
     preds = np.stack(preds)                           # [M, N, 1] fp64
+    preds_bf = np.stack(preds_bf)
     labels = np.vstack(ys).astype(np.float32)
     ens = preds.astype(np.float32).mean(axis=0)       # evaluate.py: np.mean of float32 predictions
     thr = MR.generate_thresholds(200, 1e-7) + [0.5]
     tp, fp, fn, tn = MR.counts_at_thresholds(labels, ens, thr)
     spec, sens = MR.spec_sens(tp, fp, fn, tn)
+    ens_bf = preds_bf.astype(np.float32).mean(axis=0)
     np.savez_compressed(os.path.join(OUT, "eval_res299_b32.npz"), preds=preds, labels=labels, ens=ens,
+                        preds_bf16emu=preds_bf, auc_bf16emu=np.array(MR.auc(labels, ens_bf)),
+                        brier_bf16emu=np.array(MR.brier(labels, ens_bf)),
                         input_sha256=np.array(digest), auc=np.array(MR.auc(labels, ens)),
                         brier=np.array(MR.brier(labels, ens)), confusion=MR.confusion_matrix(tp[-1], fp[-1], fn[-1],
                                                                                              tn[-1]),
@@ -259,6 +268,17 @@ def main():
         curve["losses_bf16emu"] = _net(299, 16, 0, steps=100, cycle=32, bf16=True)["losses"]
         np.savez_compressed(p, **curve)
         print(f"curve16bf: {time.time() - t0:.0f}s", flush=True)
+    if "curve16bf32" in todo:
+        # a SECOND independent bf16 implementation of the same 100 steps: bf16
+        # storage emulated as above but every product summed in fp32 (the
+        # GPU's accumulation precision) instead of fp64.  The spread between
+        # the two emulations calibrates the bf16 curve test's per-step bar
+        #  without reference to any GPU run.
+        p = os.path.join(OUT, "loss_curve_res299_b16.npz")
+        curve = dict(np.load(p))
+        curve["losses_bf16emu32"] = _net(299, 16, 0, steps=100, cycle=32, dtype="float32", bf16=True)["losses"]
+        np.savez_compressed(p, **curve)
+        print(f"curve16bf32: {time.time() - t0:.0f}s", flush=True)
     if "eval299" in todo:
         eval299()
         print(f"eval299: {time.time() - t0:.0f}s", flush=True)

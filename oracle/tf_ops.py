@@ -207,16 +207,28 @@ def momentum(w, g, a, lr=3e-3, m=0.9):
     return w - a * lr, a
 
 
+def adam_beta_powers(t, b1=0.9, b2=0.999):
+    """TF AdamOptimizer's fp32 beta1_power / beta2_power variables at step t
+    (1-based): initialised to beta (fp32), multiplied by beta (fp32) after
+    each step (optimizer._finish)."""
+    f = np.float32
+    p1, p2 = f(b1), f(b2)
+    for _ in range(t - 1):
+        p1, p2 = f(p1 * f(b1)), f(p2 * f(b2))
+    return p1, p2
+
+
 def adam_f32(w, g, m, v, t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8):
     """TF AdamOptimizer -> ApplyAdam (north-star extra; not used by the
     reference), restated in IEEE fp32 in TF's operation order (Eigen, no
     fused multiply-add): m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2);
-    var -= (m * alpha) / (sqrt(v) + eps), alpha = lr sqrt(1 - b2^t) / (1 - b1^t)
-    (computed in fp64 then rounded, as the host passes it).  Returns
-    (w, m, v, alpha) as float32."""
+    var -= (m * alpha) / (sqrt(v) + eps), alpha = lr * sqrt(1 - beta2_power) /
+    (1 - beta1_power) in fp32, left to right, from the fp32 beta-power
+    variables (adam_beta_powers).  Returns (w, m, v, alpha) as float32."""
     f = np.float32
     w, g, m, v = (np.asarray(a, np.float32) for a in (w, g, m, v))
-    alpha = f(lr * np.sqrt(1 - b2 ** t) / (1 - b1 ** t))
+    p1, p2 = adam_beta_powers(t, b1, b2)
+    alpha = f(f(f(lr) * np.sqrt(f(1) - p2)) / (f(1) - p1))
     one_b1, one_b2 = f(1) - f(b1), f(1) - f(b2)
     m = m + (g - m) * one_b1
     v = v + (g * g - v) * one_b2

@@ -34,15 +34,15 @@ def _shard(step, rank):
     return synth.fundus_batch(k, B, RES), synth.labels(k, B, p=0.5)
 
 
-def _rank(rank, port, outdir):
+def _rank(rank, port, outdir, dtype="f32", payload="f32"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     from jr.dist import BucketAllReduce
     from jr.engine import Engine
-    eng = Engine(B, RES, RES, seed=3, autotune=False)
-    ar = BucketAllReduce(eng, WORLD, bucket_bytes=8 << 20)
+    eng = Engine(B, RES, RES, seed=3, autotune=False, dtype=dtype)
+    ar = BucketAllReduce(eng, WORLD, bucket_bytes=8 << 20, payload=payload)
     losses = []
     for step in range(STEPS):
         eng.set_batch(*_shard(step, rank))
@@ -56,13 +56,19 @@ def _rank(rank, port, outdir):
     dist.destroy_process_group()
 
 
-def test_two_ranks_equal_one_process_averaging_shards():
+@pytest.mark.parametrize("dtype,payload", [("f32", "f32"), ("bf16", "f32"), ("bf16", "bf16")])
+def test_two_ranks_equal_one_process_averaging_shards(dtype, payload):
+    """fp32 and bf16 engines (configs 2 and 3), fp32 or bf16 gradient payload.
+    The one-process reference sums the two shards' gradients exactly as the
+    two-rank all-reduce does: fp32 a + b, or (bf16 payload) each shard's
+    gradient rounded to bf16, added, the sum rounded to bf16 (gloo / RCCL sum
+    bf16 values in fp32 -- exact for two terms -- and store bf16)."""
     import torch.multiprocessing as mp
     from jr.engine import Engine
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.get_context("spawn")
-        ps = [ctx.Process(target=_rank, args=(r, port, d)) for r in range(WORLD)]
+        ps = [ctx.Process(target=_rank, args=(r, port, d, dtype, payload)) for r in range(WORLD)]
         for p in ps:
             p.start()
         for p in ps:
@@ -71,7 +77,7 @@ def test_two_ranks_equal_one_process_averaging_shards():
         got = [np.load(os.path.join(d, f"params{r}.npy")) for r in range(WORLD)]
         got_losses = [np.load(os.path.join(d, f"losses{r}.npy")) for r in range(WORLD)]
         got_g0 = [np.load(os.path.join(d, f"grad{r}.npy")) for r in range(WORLD)]
-    ref = Engine(B, RES, RES, seed=3, autotune=False)
+    ref = Engine(B, RES, RES, seed=3, autotune=False, dtype=dtype)
     ref_losses = [[], []]
     for step in range(STEPS):
         gsum = None
@@ -82,7 +88,11 @@ def test_two_ranks_equal_one_process_averaging_shards():
             ref.synchronize()
             ref_losses[r].append(ref.loss_value())
             g = ref.grads.clone()
+            if payload == "bf16":
+                g = g.to(torch.bfloat16).float()
             gsum = g if gsum is None else gsum + g
+        if payload == "bf16":
+            gsum = gsum.to(torch.bfloat16).float()
         ref.grads.copy_(gsum)
         torch.cuda.synchronize()          # copy_ ran on torch's stream, the update runs on the engine's
         if step == 0:

@@ -4,7 +4,7 @@ Stamps in jr_conv_impl.h): where a block's cycles go (prologue = ring fill up
 to the first barrier, K loop, of which vmcnt waits + barriers, epilogue), how
 many blocks share a CU over the launch, and the clock the chip held.
 Diagnostic only (the stamps cost a few % of the loop).
-  python tools/conv_stamps.py <dtype 1|3> <op 0|1|2> <layer> <cfg> [reps]"""
+  python tools/conv_stamps.py <dtype 0|1|2|3> <op 0|1|2> <layer> <cfg> [reps]"""
 import ctypes
 import os
 import sys
@@ -21,7 +21,8 @@ from jr import _ffi  # noqa: E402
 LAYERS = {"c17x7": (64, 17, 17, 192, 192, 1, 7, 1, 0, 3), "c17x1": (64, 17, 17, 768, 192, 1, 1, 1, 0, 0),
           "c35x3": (64, 35, 35, 64, 96, 3, 3, 1, 1, 1), "c8x3": (64, 8, 8, 384, 384, 1, 3, 1, 0, 1),
           "conv5": (64, 73, 73, 80, 192, 3, 3, 1, 0, 0), "conv3": (64, 147, 147, 32, 64, 3, 3, 1, 1, 1),
-          "c8x33": (64, 8, 8, 448, 384, 3, 3, 1, 1, 1), "m17": (64, 17, 17, 768, 512, 1, 1, 1, 0, 0)}
+          "c8x33": (64, 8, 8, 448, 384, 3, 3, 1, 1, 1), "m17": (64, 17, 17, 768, 512, 1, 1, 1, 0, 0),
+          "c35x5": (64, 35, 35, 48, 64, 5, 5, 1, 2, 2), "c8x1": (64, 8, 8, 2048, 1152, 1, 1, 1, 0, 0)}
 
 
 def main():
@@ -33,12 +34,14 @@ def main():
     L.jr_debug_set_stamps.argtypes = [ctypes.c_void_p]
     n, h, w, ci, co, kh, kw, s, ph, pw = LAYERS[layer]
     ho, wo = (h + 2 * ph - kh) // s + 1, (w + 2 * pw - kw) // s + 1
-    cs = (ci + 7) // 8 * 8
+    q = 8 if dt in (1, 3) else 4
+    cs = (ci + q - 1) // q * q
     d = _ffi.ConvDesc(n, h, w, ci, co, kh, kw, s, s, ph, pw, ho, wo, 0, cs, 0, co)
     pl = 3 if dt == 3 else 1
-    x = torch.randn(pl * n * h * w * cs, device="cuda").to(torch.bfloat16)
-    wt = (torch.randn(pl * kh * kw * cs * co, device="cuda") * 0.05).to(torch.bfloat16)
-    dy = torch.randn(pl * n * ho * wo * co, device="cuda").to(torch.bfloat16)
+    et = torch.bfloat16 if dt in (1, 3) else torch.float32
+    x = torch.randn(pl * n * h * w * cs, device="cuda").to(et)
+    wt = (torch.randn(pl * kh * kw * cs * co, device="cuda") * 0.05).to(et)
+    dy = torch.randn(pl * n * ho * wo * co, device="cuda").to(et)
     ot = torch.bfloat16 if dt == 1 else torch.float32
     y = torch.zeros(n * ho * wo * co, device="cuda", dtype=ot)
     dx = torch.zeros(n * h * w * cs, device="cuda", dtype=ot)

@@ -32,7 +32,13 @@ REPS = 3
 def tune(dtype, math, B, res, train):
     eng = Engine(B, res, res, dtype=dtype, conv_math=math, train=train, autotune=False)
     eng.clear_tile_table()
-    eng.autotune()
+    n = [0]
+
+    def tick(name):     # a line every few units: the GPU box kills a run silent for 3 minutes
+        n[0] += 1
+        if n[0] % 8 == 0:
+            print(f"    {math} B={B} {res}^2: unit {n[0]} {name}", flush=True)
+    eng.autotune(progress=tick)
     t = eng.tile_table()
     t["train"] = train
     eng.clear_tile_table()
@@ -44,13 +50,18 @@ def tune(dtype, math, B, res, train):
 def main():
     default = os.path.join(ROOT, "jama16-retina-replication_amd", "jr", "tiles_mi355x.json")
     out = sys.argv[1] if len(sys.argv) > 1 else default
+    # selectors: a conv math ("bf16") or one workload "math:batch:res:train" ("bf16:64:587:1")
     only = set(sys.argv[2:])
+    sel = lambda w: (not only) or w[1] in only or f"{w[1]}:{w[2]}:{w[3]}:{int(w[4])}" in only  # noqa: E731
+    key = lambda t: (t["conv_math"], t["batch"], t["height"], t["train"])  # noqa: E731
     tables = []
     if only:
-        with open(default) as f:
-            tables = [t for t in json.load(f)["tables"] if t["conv_math"] not in only]
+        src = out if os.path.exists(out) else default   # resume into an existing output file
+        with open(src) as f:
+            tables = [t for t in json.load(f)["tables"]
+                      if not any(sel(w) and key(t) == (w[1], w[2], w[3], w[4]) for w in WORKLOADS)]
     for w in WORKLOADS:
-        if only and w[1] not in only:
+        if not sel(w):
             continue
         t0 = time.time()
         runs = []
@@ -68,9 +79,9 @@ def main():
         t["configs"] = cfg
         tables.append(t)
         print(f"{w}: {len(cfg)} launches tuned x{REPS} in {time.time() - t0:.0f} s", flush=True)
-    with open(out, "w") as f:
-        json.dump({"device": torch.cuda.get_device_name(0), "tables": tables}, f, indent=1, sort_keys=True)
-    print("wrote", out)
+        with open(out, "w") as f:     # after every workload: a run cut short keeps what it finished
+            json.dump({"device": torch.cuda.get_device_name(0), "tables": tables}, f, indent=1, sort_keys=True)
+        print("wrote", out, flush=True)
 
 
 if __name__ == "__main__":
