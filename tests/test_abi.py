@@ -87,10 +87,11 @@ def test_crc32c_known_answers():
 
 
 def test_no_cpu_fallback_when_library_missing(monkeypatch, tmp_path):
-    import importlib
     from jr import _ffi
     monkeypatch.setattr(_ffi, "_lib", None)
     monkeypatch.setattr(_ffi, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.delenv("JR_LIB_DIAG", raising=False)
     with pytest.raises(ImportError):
         _ffi.load()
-    importlib.reload(_ffi)
+    # (monkeypatch restores _lib and LIB_PATH; no module reload, which would
+    # leave the restored library bound to the old module's ctypes classes)
