@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(W * 64) k_stream(const char* __restrict__ src,
   uint4 acc = make_uint4(0, 0, 0, 0);
   for (int i = 0; i < iters; ++i) {
     unsigned lo;
-    if (MODE == 2) {
+    if (MODE == 2 || MODE == 3) {
       // 1024 / RB rows of RB bytes per instruction, rows RS bytes apart
       // (RB = 64, RS = 160: a BK = 32 bf16 K-tile row set of conv5, c_in 80)
       lo = (lane / (RB / 16)) * RS + (lane % (RB / 16)) * 16;
@@ -56,7 +56,15 @@ __global__ void __launch_bounds__(W * 64) k_stream(const char* __restrict__ src,
       lo = lane * 16;
     }
     const char* p = src + ((off + lo) & (kRegion - 1));
-    if (MODE == 1) {   // D independent loads in flight, then fold
+    if (MODE == 3 && (wave & 1)) {   // mixed: odd waves register loads, even waves LDS-DMA
+      uint4 v[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) v[d] = *reinterpret_cast<const uint4*>(src + ((off + lo + d * 1024u) & (kRegion - 1)));
+#pragma unroll
+      for (int d = 0; d < D; ++d) { acc.x ^= v[d].x; acc.y ^= v[d].y; acc.z ^= v[d].z; acc.w ^= v[d].w; }
+      i += D - 1;
+      off = (off + (D - 1) * 1024u) & (kRegion - 1);
+    } else if (MODE == 1) {   // D independent loads in flight, then fold
       uint4 v[D];
 #pragma unroll
       for (int d = 0; d < D; ++d) v[d] = *reinterpret_cast<const uint4*>(src + ((off + lo + d * 1024u) & (kRegion - 1)));
@@ -69,10 +77,10 @@ __global__ void __launch_bounds__(W * 64) k_stream(const char* __restrict__ src,
                                        (__attribute__((address_space(3))) void*)(myring + (i % D) * 1024), 16, 0, 0);
       wait_vm(D - 1);
     }
-    off = (off + (MODE == 2 ? (unsigned)(1024 / RB * RS) : 1024u)) & (kRegion - 1);
+    off = (off + (MODE >= 2 ? (unsigned)(1024 / RB * RS) : 1024u)) & (kRegion - 1);
   }
   wait_vm(0);
-  if (MODE == 1) {
+  if (MODE == 1 || (MODE == 3 && (wave & 1))) {
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[0] = 1;   // keeps the loads live
   } else if (lane == 0) {
     out[gw & 1023] = *reinterpret_cast<const unsigned*>(myring);
@@ -101,7 +109,7 @@ static void run(const char* src, unsigned* out, int bpc, int cus) {
   const double bytes = (double)grid * W * iters * 1024.0;
   const double gbs_cu = bytes / (best * 1e-3) / cus / 1e9;
   const int mode_loads = D;
-  if (MODE == 2) printf("[rows of %3d B, %4d B apart] ", RB, RS);
+  if (MODE >= 2) printf("[rows of %3d B, %4d B apart] ", RB, RS);
   printf("mode %d  waves/block %d  blocks/CU %d  in-flight/wave %2d  KiB in flight/CU %4d  %7.1f us  %6.1f GB/s per CU  %6.2f TB/s chip\n",
          MODE, W, bpc, mode_loads, W * D * bpc, best * 1e3, gbs_cu, gbs_cu * cus / 1e3);
   CHECK(hipEventDestroy(e0));
@@ -150,6 +158,13 @@ int main() {
   run<2, 8, 8, 256, 320>(src, out, 1, cus);
   run<2, 4, 8, 128, 256>(src, out, 2, cus);
   run<2, 4, 8, 64, 128>(src, out, 2, cus);
+  // mixed: half the waves LDS-DMA, half register loads (do the two paths share the TA?)
+  run<3, 8, 8, 128, 128>(src, out, 1, cus);
+  run<3, 8, 8, 128, 256>(src, out, 1, cus);
+  run<3, 8, 8, 64, 128>(src, out, 1, cus);
+  run<3, 8, 16, 128, 256>(src, out, 1, cus);
+  run<3, 4, 8, 128, 256>(src, out, 2, cus);
+  // register loads with the row geometry (mode 1 is contiguous)
   // register loads
   run<1, 4, 4>(src, out, 1, cus);
   run<1, 4, 8>(src, out, 1, cus);
