@@ -120,9 +120,10 @@ def test_cli_two_ranks_equal_one_rank(evalset):
                  "--master-addr", "127.0.0.1", "--master-port", str(port), ev, "-o", "--data_dir", data,
                  "-lm", lm, "-so", two_csv, "-b", str(B)],
                 {"JR_DIST_BACKEND": "gloo", "JR_ONE_DEVICE": "1"}, str(d))
-    # (gloo's own connection log lines, printed by every rank, are not evaluate.py output)
+    # (gloo's own connection log lines, printed by every rank, are not evaluate.py output; they
+    # can also leave a stray blank line, so blank lines are not compared either)
     strip = lambda s: [ln for ln in s.splitlines() if "Saving operating" not in ln and "amdgpu.ids" not in ln  # noqa: E731
-                       and not ln.startswith("[Gloo]")]
+                       and not ln.startswith("[Gloo]") and ln.strip()]
     assert strip(out1) == strip(out2), (out1, out2)
     assert open(one_csv).read() == open(two_csv).read()
     assert "AUC:" in out1
