@@ -158,7 +158,8 @@ int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const void* a, 
                        void* ws, size_t ws_bytes, void* stream);
 /* Tile configuration the next call would use (DGRAD: per stride phase),
  * and an explicit override (reproducibility, tests).  A config id is
- * tile | (splits << 8), splits = 0: planner's split-K factor; set_config
+ * tile | (splits << 8), splits = 0: planner's split-K factor (at most
+ * 1024); set_config
  * with cfg = -1 drops the override (autotuned or set) for that GEMM. */
 int jr_conv2d_get_config(const jr_conv_desc* d, int op, int dtype, int phase);
 int jr_conv2d_set_config(const jr_conv_desc* d, int op, int dtype, int phase, int cfg);

@@ -645,6 +645,9 @@ struct Phase {
 // A config id is tile | (splits << 8): splits == 0 lets the planner pick
 // the split-K factor, otherwise it is forced (autotuning explores both).
 constexpr int kSplitShift = 8;
+// split-K factors up to 1024: the stem filter gradients (3 tiles of M = 288,
+// K = 1.4 M pixels) still gain from 256 to 512 slabs (more resident blocks)
+constexpr int kMaxSplits = 1024;
 static int cfg_tile(int cfg) { return cfg & ((1 << kSplitShift) - 1); }
 static int cfg_splits(int cfg) { return cfg >> kSplitShift; }
 
@@ -1192,7 +1195,7 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
       const Plan dp = plan_with(dtype, c, M, N, K);
       int prev = -1;
       for (int v : {1, dp.splits / 4, dp.splits / 2, dp.splits * 2}) {
-        if (v < 1 || v == dp.splits || v == prev || v > 256 || v > dp.ktiles) continue;
+        if (v < 1 || v == dp.splits || v == prev || v > kMaxSplits || v > dp.ktiles) continue;
         prev = v;
         time_cfg(c | (v << kSplitShift));
         if (rc) break;
@@ -1459,7 +1462,7 @@ JR_API int jr_conv2d_debug_time(const jr_conv_desc* d, int cfg, int dbg, const v
 JR_API int jr_conv2d_set_config(const jr_conv_desc* d, int op, int dtype, int phase, int cfg) {
   int rc = validate(d, op, dtype);
   if (rc) return rc;
-  if (cfg < -1 || (cfg >= 0 && (cfg_tile(cfg) >= cfg_count(dtype) || cfg_splits(cfg) > 256)))
+  if (cfg < -1 || (cfg >= 0 && (cfg_tile(cfg) >= cfg_count(dtype) || cfg_splits(cfg) > kMaxSplits)))
     return fail(JR_ERR_INVALID, "conv set_config: bad config index");
   Phase ph[64];
   int nph = 1;

@@ -59,7 +59,7 @@ flops = 2.0 * n * ho * wo * co * kh * kw * ci
 nph = s * s if op == 1 else 1
 res = []
 for tile in range(L.jr_conv2d_num_configs(dt)):
-    for sp in (1, 2, 3, 4, 6, 8, 12, 16, 32, 64, 128, 256):
+    for sp in (1, 2, 3, 4, 6, 8, 12, 16, 32, 64, 128, 256, 512, 1024):
         cfg = tile | (sp << 8)
         ok = all(L.jr_conv2d_set_config(ctypes.byref(d), op, dt, p, cfg) == 0 for p in range(nph))
         if not ok or (L.jr_conv2d_get_config(ctypes.byref(d), op, dt, 0) & 255) != tile or run() != 0:
