@@ -21,7 +21,8 @@ LAYERS = {"c17x7": (64, 17, 17, 192, 192, 1, 7, 1, 0, 3), "c17x1": (64, 17, 17, 
           "conv5": (64, 73, 73, 80, 192, 3, 3, 1, 0, 0), "conv1": (64, 299, 299, 3, 32, 3, 3, 2, 0, 0),
           "conv2": (64, 149, 149, 32, 32, 3, 3, 1, 0, 0), "conv3": (64, 147, 147, 32, 64, 3, 3, 1, 1, 1),
           "c17x7v": (64, 17, 17, 192, 192, 7, 1, 1, 3, 0), "c8x3v": (64, 8, 8, 384, 384, 3, 1, 1, 1, 0),
-          "c8x33": (64, 8, 8, 448, 384, 3, 3, 1, 1, 1), "c35x33": (64, 35, 35, 96, 96, 3, 3, 1, 1, 1)}
+          "c8x33": (64, 8, 8, 448, 384, 3, 3, 1, 1, 1), "c35x33": (64, 35, 35, 96, 96, 3, 3, 1, 1, 1),
+          "c35p192": (64, 35, 35, 192, 32, 1, 1, 1, 0, 0), "c35p288": (64, 35, 35, 288, 64, 1, 1, 1, 0, 0)}
 dt, op, layer = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
 reps = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 _ffi.init(0)

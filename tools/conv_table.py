@@ -14,7 +14,10 @@ B = int(args[1]) if len(args) > 1 else 64
 res = int(args[6]) if len(args) > 6 else 299
 sys.argv = [sys.argv[0]] + args
 rows = [r for r in csv.DictReader(open(trace)) if r["Kind"] == "KERNEL_DISPATCH"]
-rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+# host issue order (Dispatch_Id), not start time: with several lanes the GPU
+# starts kernels of different streams out of issue order, and matching by start
+# time mislabels the launches of parallel branches (round-3 tables before r03e)
+rows.sort(key=lambda r: int(r["Dispatch_Id"]) if r.get("Dispatch_Id") else int(r["Start_Timestamp"]))
 g = build_inception_v3(res, res)
 plan = build_plan(g, "--unfused" not in sys.argv[0:] and "--unfused" not in os.environ.get("CONV_TABLE", ""))
 
@@ -130,7 +133,7 @@ opt = [i for i, r in enumerate(rows) if "k_nesterov" in r["Kernel_Name"] or "k_s
 if len(opt) >= 2:
     a, b = opt[-2] + 1, opt[-1] + 1
     step = rows[a:b]
-    t0 = int(step[0]["Start_Timestamp"]); t1 = int(step[-1]["End_Timestamp"])
+    t0 = min(int(r["Start_Timestamp"]) for r in step); t1 = max(int(r["End_Timestamp"]) for r in step)
     from collections import defaultdict
     cat = defaultdict(float)
     for r in step:
