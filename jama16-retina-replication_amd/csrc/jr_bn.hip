@@ -29,6 +29,10 @@ namespace jr {
 #define JR_BN_BWD_ROWS 8
 #endif
 constexpr int kMaxChunks = JR_BN_MAX_CHUNKS;  // partial sums per channel (finalize reads them)
+#ifndef JR_BN_F32_SELECT
+#define JR_BN_F32_SELECT 0
+#endif
+constexpr bool kF32Select = JR_BN_F32_SELECT;  // (diagnostic) fp32 reduce loads in the select form
 // rows in flight per thread in the reductions (16 B per row and operand)
 template <int MODE> constexpr int red_rows() { return MODE == 0 ? 16 : JR_BN_BWD_ROWS; }
 #ifndef JR_BN_APP_UNROLL
@@ -146,7 +150,8 @@ __device__ __forceinline__ int seg_of(const BnSegs& sg, int ch) {
 // per thread: the loop is latency-bound, not bandwidth-bound, with fewer.
 // Partials: part[2][c][nchunks] (fp64, chunk-contiguous for the finalize).
 template <int MODE, typename T>
-__global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int xs, BnSegs sg, int64_t m, int c,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
+k_bn_reduce(const T* __restrict__ x, int xs, BnSegs sg, int64_t m, int c,
                                                    int rows_per_chunk, const float* __restrict__ mean,
                                                    const float* __restrict__ invstd, double* part) {
   constexpr int VW = Vec<T>::N;
@@ -183,16 +188,14 @@ __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int 
       uint4 xr[U], gr[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        // Rows past the chunk add zero bits (= 0.0 in both dtypes).  bf16:
-        // load the chunk's last row (always valid) and zero after the load --
-        // the select form below compiles to a FLAT load from a select of the
-        // row address and a scratch copy of the zero constant (scratch store
-        // per row), which measured 6 % slower for bf16 (bnbench); for fp32
-        // the select form measured faster (stem shapes 3-6 %, step 1.50 vs
-        // 1.75 ms), so each dtype keeps its faster form.
+        // Rows past the chunk add zero bits (= 0.0 in both dtypes): load the
+        // chunk's last row (always valid) and zero after the load.  The
+        // select form (JR_BN_F32_SELECT, the fp32 default before the pins
+        // below) compiles to a FLAT load from a select of the row address
+        // and a scratch copy of the zero constant, a branch and a wait per row.
         const int64_t ri = r + (int64_t)u * rpp;
         const uint4 z = make_uint4(0, 0, 0, 0);
-        if constexpr (sizeof(T) == 4) {
+        if constexpr (sizeof(T) == 4 && kF32Select) {
           xr[u] = ri < r1 ? *reinterpret_cast<const uint4*>(xp + ri * xs) : z;
           if (MODE == 1) gr[u] = ri < r1 ? *reinterpret_cast<const uint4*>(gp + ri * dy_stride) : z;
         } else {
@@ -205,6 +208,14 @@ __global__ void __launch_bounds__(256) k_bn_reduce(const T* __restrict__ x, int 
             gr[u] = in ? gv : z;
           }
         }
+      }
+      // all 2U loads in flight before the first use: without the pins hipcc
+      // issued half of them one at a time, each behind vmcnt(0) (a memory
+      // round trip per row: the 17^2 / 8^2 reduces took 14-16 us)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        pin(xr[u]);
+        if (MODE == 1) pin(gr[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {

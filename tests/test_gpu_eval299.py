@@ -116,12 +116,18 @@ def test_cli_two_ranks_equal_one_rank(evalset):
     one_csv, two_csv = str(d / "one.csv"), str(d / "two.csv")
     out1 = _cli([sys.executable, ev, "-o", "--data_dir", data, "-lm", lm, "-so", one_csv, "-b", str(B)], {}, str(d))
     port = 29500 + os.getpid() % 1000
-    out2 = _cli([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                 "--master-addr", "127.0.0.1", "--master-port", str(port), ev, "-o", "--data_dir", data,
-                 "-lm", lm, "-so", two_csv, "-b", str(B)],
-                {"JR_DIST_BACKEND": "gloo", "JR_ONE_DEVICE": "1"}, str(d))
-    # (gloo's own connection log lines, printed by every rank, are not evaluate.py output; they
-    # can also leave a stray blank line, so blank lines are not compared either)
+    # each rank's stdout to its own file (--redirects): on the shared stream
+    # rank 1's gloo connection line could be split by rank 0's output
+    logs = d / "torchrun_logs"
+    _cli([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+          "--master-addr", "127.0.0.1", "--master-port", str(port), "--log-dir", str(logs), "--redirects", "3",
+          ev, "-o", "--data_dir", data, "-lm", lm, "-so", two_csv, "-b", str(B)],
+         {"JR_DIST_BACKEND": "gloo", "JR_ONE_DEVICE": "1"}, str(d))
+    rank0 = list(logs.glob("*/attempt_*/0/stdout.log"))
+    assert len(rank0) == 1, rank0
+    out2 = rank0[0].read_text()
+    # (gloo's own connection log line is not evaluate.py output; blank lines
+    # are not compared either)
     strip = lambda s: [ln for ln in s.splitlines() if "Saving operating" not in ln and "amdgpu.ids" not in ln  # noqa: E731
                        and not ln.startswith("[Gloo]") and ln.strip()]
     assert strip(out1) == strip(out2), (out1, out2)
