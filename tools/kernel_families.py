@@ -30,9 +30,14 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     opt = [i for i, r in enumerate(rows) if "k_nesterov" in r[2]]
-    if len(opt) < nsteps + 1:
-        sys.exit(f"need {nsteps + 1} optimizer launches, found {len(opt)}")
-    win = rows[opt[-nsteps - 1] + 1:opt[-1] + 1]
+    # whole training steps only: bench.py's per-family rate replays after the
+    # timed region also launch the optimizer alone, so keep the windows
+    # between optimizer launches that hold conv kernels
+    steps = [(a, b) for a, b in zip(opt, opt[1:])
+             if any("k_conv" in rows[i][2] for i in range(a + 1, b))]
+    if len(steps) < nsteps:
+        sys.exit(f"need {nsteps} whole steps, found {len(steps)}")
+    win = [r for a, b in steps[-nsteps:] for r in rows[a + 1:b + 1]]
     t = defaultdict(int)
     c = defaultdict(int)
     for s, e, n in win:
