@@ -11,7 +11,9 @@
 // backward kernels and be captured in a HIP graph.  The unique id is either
 // passed in (exchanged by the caller's own bootstrap) or handed over through
 // a file tagged with the caller's run id (rank 0 writes it with an atomic
-// rename, the others poll for the file of their run).
+// rename, the others poll for the file of their run; rank 0 removes it once
+// the communicator exists).  The run id must be unique per job: torchrun's
+// default TORCHELASTIC_RUN_ID is the literal "none" for every job.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -115,7 +117,11 @@ JR_API int jr_comm_init_file(int rank, int world, const char* uid_path, const ch
       std::this_thread::sleep_for(std::chrono::milliseconds(10));
     }
   }
-  return jr_comm_init(rank, world, id, device, out);
+  const int rc = jr_comm_init(rank, world, id, device, out);
+  // ncclCommInitRank is collective: when it returns on rank 0 every rank has
+  // read the id, so the file is removed and no later job can find it
+  if (rank == 0) std::remove(path.c_str());
+  return rc;
 }
 
 JR_API int jr_allreduce_sum(jr_comm* comm, void* buf, size_t n, int dtype, void* stream) {

@@ -63,6 +63,33 @@ def make_buckets(layout, total: int, bucket_bytes: int = DEFAULT_BUCKET_BYTES) -
     return buckets
 
 
+def resolve_run_id(run_id: Optional[str] = None) -> str:
+    """The id that tags the RCCL unique-id file of THIS job (jr_comm_init_file).
+
+    It must differ from every earlier job's, or a rank may join an id file an
+    earlier job left at the same path.  In order:
+      * an explicit run_id;
+      * a nonce rank 0 draws and broadcasts over an initialised
+        torch.distributed group (unique per job and per restart);
+      * the launcher's TORCHELASTIC_RUN_ID + TORCHELASTIC_RESTART_COUNT, but
+        never torchrun's default id, the literal "none", which every job that
+        passes no --rdzv-id shares;
+    otherwise ValueError.  MASTER_ADDR:MASTER_PORT is not used: a fixed port
+    repeats from job to job."""
+    if run_id:
+        return str(run_id)
+    if dist.is_available() and dist.is_initialized():
+        box = [os.urandom(16).hex() if dist.get_rank() == 0 else None]
+        dist.broadcast_object_list(box, 0)
+        return f"nonce-{box[0]}"
+    rid = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    if rid and rid.lower() != "none":
+        return f"{rid}#{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
+    raise ValueError("JrComm(uid_path=...) needs a run id unique to this job: pass run_id, initialise "
+                     "torch.distributed (rank 0 broadcasts a nonce), or launch with an explicit "
+                     "--rdzv-id (TORCHELASTIC_RUN_ID is 'none' by default)")
+
+
 class JrComm:
     """libjr's RCCL communicator (one per process / GPU)."""
 
@@ -72,13 +99,9 @@ class JrComm:
         self.h = ctypes.c_void_p()
         if uid_path is not None:
             # the id file is tagged with the job's run id: a file an earlier job
-            # left at uid_path is ignored (default: the launcher's rendezvous id)
-            run_id = run_id or os.environ.get("TORCHELASTIC_RUN_ID") or (
-                f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}"
-                if "MASTER_ADDR" in os.environ and "MASTER_PORT" in os.environ else None)
-            if not run_id:
-                raise ValueError("JrComm(uid_path=...) needs a run_id shared by every rank of the job "
-                                 "(or TORCHELASTIC_RUN_ID / MASTER_ADDR+MASTER_PORT in the environment)")
+            # left at uid_path is ignored; rank 0 removes the file once the
+            # communicator exists (jr_comm_init_file)
+            run_id = resolve_run_id(run_id)
             _ffi.check("jr_comm_init_file", self.lib.jr_comm_init_file(rank, world, uid_path.encode(),
                                                                         run_id.encode(), device, timeout_ms,
                                                                         ctypes.byref(self.h)))

@@ -426,6 +426,13 @@ class Engine:
         if self.train_mode:
             self.accum.zero_()
             self.grads.zero_()
+            # optimizer state restarts with the parameters: Adam's v slot and
+            # its fp32 beta powers (TF initialises beta1_power / beta2_power to
+            # beta1 / beta2 with the slots)
+            if self.adam_v is not None:
+                self.adam_v.zero_()
+            self.adam_t = 0
+            self.adam_b1p, self.adam_b2p = np.float32(self.adam_b1), np.float32(self.adam_b2)
 
     def params_numpy(self) -> np.ndarray:
         """Parameters in the Keras layout (checkpoints, the oracle)."""

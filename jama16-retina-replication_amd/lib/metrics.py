@@ -9,7 +9,7 @@ callables on a host-side streaming state:
     reset()                      -> tf.variables_initializer(local vars)
 `metric` is one of the tf.metrics restatements below (same names and
 keyword arguments as the TF functions the reference passes: train.py:156-180,
-evaluate.py:432-462): labels/predictions given at construction are ignored
+evaluate.py:128-161): labels/predictions given at construction are ignored
 (they were graph tensors); the batch arrays are passed to update().
 
 Arithmetic follows [TF-3P] metrics_impl: `_confusion_matrix_at_thresholds`

@@ -68,9 +68,15 @@ def build_parser():
     p.add_argument("--image_size", type=int, default=299, help="input resolution (299; 587 high-res variant)")
     p.add_argument("--num_epochs", type=int, default=NUM_EPOCHS)
     p.add_argument("--seed", type=int, default=0, help="weight init seed (ensemble member index)")
+    p.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
+                   help="activation storage and conv arithmetic: f32 (the reference's; default) or bf16 MFMA "
+                        "(BASELINE configs 3 and 5; parameters, gradients, momentum and BN statistics stay fp32)")
     p.add_argument("--conv_math", default="x8", choices=["x8", "x8p", "f32"],
-                   help="fp32 convolution arithmetic: x8 = exact 3-way bf16 split on the matrix cores (fp32-accurate, "
-                        "default), x8p = the same on pre-split operand planes, f32 = fp32 MFMA")
+                   help="fp32 convolution arithmetic (--dtype f32): x8 = exact 3-way bf16 split on the matrix cores "
+                        "(fp32-accurate, default), x8p = the same on pre-split operand planes, f32 = fp32 MFMA")
+    p.add_argument("--replica_dump_dir", default=None,
+                   help="(data parallel check) every rank writes its parameters after each epoch as "
+                        "<dir>/params_e<epoch>_r<rank>.npy (Keras layout, fp32)")
     p.add_argument("--tiles", default="pinned", choices=["pinned", "heuristic", "autotune"],
                    help="conv tile configs: pinned (default; the committed MI355X table of this workload, "
                         "jr/tiles_mi355x.json, else the heuristic), heuristic (a function of the layer shapes only) "
@@ -123,12 +129,24 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for the N > 1 path on a one-GPU box (as evaluate.py's
+    # and bench.py's): JR_ONE_DEVICE=1 puts every rank on cuda:0,
+    # JR_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one device)
+    if os.environ.get("JR_ONE_DEVICE") == "1" or os.environ.get("JR_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("JR_DIST_BACKEND", "nccl")
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    # small host-side collectives (seed, metric sums, replica digests) run on
+    # device tensors under RCCL, host tensors under gloo
+    coll_dev = "cuda" if backend == "nccl" else "cpu"
 
     if rank == 0:
         print(f"""
@@ -144,7 +162,7 @@ Use SGD: {bool(args.vanilla_sgd)}
     size = [args.image_size, args.image_size]
     shuffle_seed = args.shuffle_seed if args.shuffle_seed is not None else int.from_bytes(os.urandom(4), "little")
     if dist:   # every rank walks the same shuffled stream of record handles
-        t = torch.tensor([shuffle_seed], dtype=torch.int64, device="cuda")
+        t = torch.tensor([shuffle_seed], dtype=torch.int64, device=coll_dev)
         dist.broadcast(t, 0)
         shuffle_seed = int(t.item())
     # data parallel: each rank decodes only its own batches (b % world ==
@@ -164,7 +182,8 @@ Use SGD: {bool(args.vanilla_sgd)}
 
     engine = Engine(max(TRAIN_BATCH_SIZE, VAL_BATCH_SIZE), args.image_size, args.image_size,
                     device=local, optimizer="sgd" if args.vanilla_sgd else ("nesterov" if USE_NESTEROV else "momentum"),
-                    lr=LEARNING_RATE, momentum=MOMENTUM, seed=args.seed, conv_math=args.conv_math,
+                    lr=LEARNING_RATE, momentum=MOMENTUM, seed=args.seed, dtype=args.dtype,
+                    conv_math=args.conv_math if args.dtype == "f32" else "bf16",
                     tiles="pinned" if args.tiles == "pinned" else "heuristic")
     table = None
     if args.tile_table:
@@ -184,10 +203,29 @@ Use SGD: {bool(args.vanilla_sgd)}
         sess.allreduce = BucketAllReduce(engine, world)
 
         def _sum_over_ranks(vec):
-            t = torch.from_numpy(vec).to("cuda")
+            t = torch.from_numpy(vec).to(coll_dev)
             dist.all_reduce(t)
             return t.cpu().numpy()
         sess.reduce = _sum_over_ranks
+
+    def check_replicas(epoch):
+        """Data parallel: every rank applies the same update to the same
+        reduced gradient, so the replicas must stay bitwise identical; compare
+        a digest of every rank's parameters once per epoch (and dump them for
+        --replica_dump_dir)."""
+        if not dist and not args.replica_dump_dir:
+            return
+        flat = engine.params_numpy()
+        if args.replica_dump_dir:
+            os.makedirs(args.replica_dump_dir, exist_ok=True)
+            np.save(os.path.join(args.replica_dump_dir, f"params_e{epoch}_r{rank}.npy"), flat)
+        if dist:
+            import hashlib
+            digest = hashlib.sha256(flat.tobytes()).hexdigest()
+            got = [None] * world
+            dist.all_gather_object(got, digest)
+            if len(set(got)) != 1:
+                raise RuntimeError(f"data-parallel replicas diverged after epoch {epoch}: {got}")
     train_writer = FileWriter(os.path.join(args.save_summaries_dir, "train")) if rank == 0 else None
 
     latest_peak_auc = 0.0
@@ -214,6 +252,7 @@ Use SGD: {bool(args.vanilla_sgd)}
         finally:
             lib.dataset.close_iterator(it)
         sess.sync_metrics("brier")
+        check_replicas(epoch)
         train_brier = sess.value("brier")
         if rank == 0:
             print("\nEnd of epoch {0}! (Brier: {1:8.6})".format(epoch, train_brier))

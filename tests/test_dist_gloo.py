@@ -84,3 +84,68 @@ def test_allreduce_world2_gloo_mean_and_overlap():
         np.testing.assert_allclose(g, want, rtol=1e-6, atol=1e-6)
         assert n_buckets >= 3 and n_issue_points >= 2      # buckets launched during backward
     np.testing.assert_array_equal(res[0][1], res[1][1])    # ranks bitwise identical
+
+
+# ---------------------------------------------------------------- JrComm run id
+def test_run_id_refuses_torchrun_default(monkeypatch):
+    """torchrun without --rdzv-id exports TORCHELASTIC_RUN_ID='none' for every
+    job: that must never tag an id file, nor MASTER_ADDR:PORT."""
+    from jr.dist import resolve_run_id
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    with pytest.raises(ValueError):
+        resolve_run_id()
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job42")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "3")
+    assert resolve_run_id() == "job42#3"
+    assert resolve_run_id("explicit") == "explicit"
+
+
+def _write_uid_file(path, run_id):
+    import struct
+    with open(path, "wb") as f:
+        f.write(b"JRCOMMID" + struct.pack("<I", len(run_id)) + run_id.encode() + bytes(128))
+
+
+def test_stale_none_tagged_id_file_is_not_joined(tmp_path, monkeypatch):
+    """A stale id file tagged 'none' (an earlier default-torchrun job) at the
+    path: under torchrun-like env vars JrComm refuses to guess a run id, and
+    libjr's rank-1 poll with this job's run id ignores the stale file and
+    times out instead of joining it (no GPU call is reached)."""
+    from jr import _ffi
+    from jr.dist import JrComm
+    uid = str(tmp_path / "jr.uid")
+    _write_uid_file(uid, "none")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    with pytest.raises(ValueError):
+        JrComm(1, 2, 0, uid_path=uid, timeout_ms=200)
+    with pytest.raises(_ffi.JRError, match="timed out"):
+        JrComm(1, 2, 0, uid_path=uid, timeout_ms=300, run_id="nonce-abc")
+
+
+def _nonce_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_RUN_ID="none")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from jr.dist import resolve_run_id
+    q.put((rank, resolve_run_id(), resolve_run_id()))
+    dist.destroy_process_group()
+
+
+def test_run_id_nonce_shared_over_group():
+    """With a torch.distributed group every rank gets rank 0's fresh nonce
+    (never 'none'); a second call draws a new one."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_nonce_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in ps])
+    for p in ps:
+        p.join(60)
+    assert res[0][1] == res[1][1] and res[0][2] == res[1][2]
+    assert res[0][1] != res[0][2] and res[0][1].startswith("nonce-") and "none" != res[0][1]
