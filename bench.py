@@ -36,7 +36,8 @@ import torch  # noqa: E402
 PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0, "x8": round(2500.0 / 8, 1), "x8p": round(2500.0 / 8, 1)}
 CONV_MATH = {"f32": "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
              "x8": "fp32 via exact 3-way bf16 split, 8 bf16 MFMAs per product (all terms > 2^-32), "
-                   "fp32 accumulate (JR_F32_X8)",
+                   "fp32 accumulate (JR_F32_X8; fwd / dgrad filters split once per step into bf16 planes, "
+                   "JR_F32_X8W, bitwise the same)",
              "x8p": "fp32 via exact 3-way bf16 split done once per operand (jr_split_x8p planes), 8 bf16 MFMAs "
                     "per product, fp32 accumulate (JR_F32_X8P)"}
 HBM_PEAK_GBS = 8000.0
@@ -80,7 +81,9 @@ def conv_roofline(eng, steps: int = 3):
     bracket every conv fwd/dgrad/wgrad call; returns (flops/step, conv s/step)."""
     from jr import _ffi
     fwd, bwd, opt, _, _ = eng._build_calls(eng.batch, 1)     # one lane: calls do not overlap
-    conv_names = {"conv_fwd", "conv_dgrad", "conv_wgrad", "wgrad_reduce"}
+    # (wprep_bf16: the per-step filter prep the conv GEMMs read -- bf16 copies,
+    # or x8's bf16 filter planes -- counted as conv time)
+    conv_names = {"conv_fwd", "conv_dgrad", "conv_wgrad", "wgrad_reduce", "wprep_bf16"}
     flops = 0
     for n in eng.g.convs:
         m = n.macs_per_image() * eng.batch

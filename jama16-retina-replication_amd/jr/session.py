@@ -32,8 +32,10 @@ class Session:
             "auc": M.create_reset_metric(M.auc, scope="auc"),
         }
         self.global_step = 0
-        # data-parallel ranks: reduce(vec float64) -> elementwise sum over ranks
+        # data-parallel ranks: reduce(vec float64) -> elementwise sum over ranks;
+        # rank: only rank 0 prints the reference's per-pass lines
         self.reduce = None
+        self.rank = 0
 
     def sync_metrics(self, *names) -> None:
         """Sum the streaming states of `names` over the ranks (collective: every

@@ -72,7 +72,10 @@ def perform_test(sess, init_op, summary_writer=None, epoch=None,
     if summary_writer is not None:
         summary_writer.add_summary({"auc": test_auc}, epoch)
 
-    print(f"Brier score: {test_brier:6.4}, AUC: {test_auc:10.8}")
-    print(f"Confusion matrix:")
-    print(test_conf_matrix[0])
+    # data parallel: one copy of the reference's lines (rank 0; every rank
+    # holds the same summed values)
+    if getattr(sess, "rank", 0) == 0:
+        print(f"Brier score: {test_brier:6.4}, AUC: {test_auc:10.8}")
+        print(f"Confusion matrix:")
+        print(test_conf_matrix[0])
     return test_auc

@@ -122,12 +122,13 @@ def main(argv=None):
     from jr.session import Session
     from jr.summary import FileWriter
 
-    print(f"Numpy version: {np.__version__}")
-    print(f"Torch version: {torch.__version__} (libjr / MI355X backend)")
     random.seed(432)                       # train.py:17
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if rank == 0:       # one copy of the reference's header lines, whatever the rank count
+        print(f"Numpy version: {np.__version__}")
+        print(f"Torch version: {torch.__version__} (libjr / MI355X backend)")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs for the N > 1 path on a one-GPU box (as evaluate.py's
     # and bench.py's): JR_ONE_DEVICE=1 puts every rank on cuda:0,
@@ -198,6 +199,7 @@ Use SGD: {bool(args.vanilla_sgd)}
     if table is not None:
         engine.set_tile_table(table)
     sess = Session(engine, thresholds, NUM_THRESHOLDS, KEPSILON)
+    sess.rank = rank
     if dist:
         from jr.dist import BucketAllReduce
         sess.allreduce = BucketAllReduce(engine, world)

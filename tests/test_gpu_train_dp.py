@@ -95,7 +95,8 @@ def test_train_cli_two_ranks(records, tmp_path, dtype):
     assert "End of epoch 0!" in stdout[0] and "End of epoch 1!" in stdout[0]
     assert "Brier score:" in stdout[0] and "AUC:" in stdout[0]
     assert "New peak auc reached" in stdout[0] or "Stopped early" in stdout[0]
-    for line in ("End of epoch", "New peak auc", "Stopped early", "Brier score:", "Training images folder"):
+    for line in ("End of epoch", "New peak auc", "Stopped early", "Brier score:", "Confusion matrix", "Numpy version",
+                 "Training images folder"):
         assert line not in stdout[1], (line, stdout[1])
     rows = open(out / "op.csv").read().strip().split("\n")
     assert rows[0] == "threshold specificity sensitivity" and len(rows) == 201
