@@ -36,8 +36,7 @@ import torch  # noqa: E402
 PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0, "x8": round(2500.0 / 8, 1), "x8p": round(2500.0 / 8, 1)}
 CONV_MATH = {"f32": "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
              "x8": "fp32 via exact 3-way bf16 split, 8 bf16 MFMAs per product (all terms > 2^-32), "
-                   "fp32 accumulate (JR_F32_X8; fwd / dgrad filters split once per step into bf16 planes, "
-                   "JR_F32_X8W, bitwise the same)",
+                   "fp32 accumulate (JR_F32_X8)",
              "x8p": "fp32 via exact 3-way bf16 split done once per operand (jr_split_x8p planes), 8 bf16 MFMAs "
                     "per product, fp32 accumulate (JR_F32_X8P)"}
 HBM_PEAK_GBS = 8000.0
@@ -51,9 +50,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None, help="per GPU (default 64 train, 32 eval)")
-    ap.add_argument("--mode", default="train", choices=["train", "eval"],
+    ap.add_argument("--mode", default="train", choices=["train", "eval", "ensemble"],
                     help="eval: forward only with batch-statistics BN, the ensemble member pass of "
-                         "evaluate.py:166-211 (BASELINE config 4)")
+                         "evaluate.py:166-211 (BASELINE config 4); ensemble: evaluate.predict_all end to end "
+                         "(TFRecord read + JPEG decode + every member's forward) over synthetic records")
+    ap.add_argument("--members", type=int, default=10, help="ensemble mode: members resident on the GPU")
+    ap.add_argument("--images", type=int, default=2048, help="ensemble mode: synthetic test images")
     ap.add_argument("--res", type=int, default=299)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--conv-math", default="x8", choices=["f32", "x8", "x8p"],
@@ -235,8 +237,88 @@ def cpu_baseline(args, res):
                       f"({dt:.1f} s)"}
 
 
+def _write_records(out_dir: str, start: int, n: int, res: int, part: int) -> None:
+    from jr import synth_records
+    synth_records.write_split(out_dir, n, size=res, p=0.079, start=start, num_shards=1, name=f"test{part:02d}")
+
+
+def ensemble_bench(args) -> dict:
+    """BASELINE config 4 on one GPU: evaluate.predict_all (the -lm ensemble
+    loop of evaluate.py: records read and decoded once per batch on the host,
+    every resident member's forward on the GPU) timed end to end over
+    synthetic fundus TFRecords, next to its two halves alone: the input
+    pipeline (decode only) and the members' forwards on resident batches."""
+    import multiprocessing as mp
+    import shutil
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "jama16-retina-replication_amd"))
+    import evaluate
+    import lib.dataset
+    from jr.engine import Engine
+    B, res, n = args.batch or 32, args.res, args.images
+    d = tempfile.mkdtemp(prefix="jr_ensemble_")
+    try:
+        parts = 8
+        per = -(-n // parts)
+        t0 = time.perf_counter()
+        with mp.get_context("spawn").Pool(parts) as pool:
+            pool.starmap(_write_records, [(d, k * per, min(per, n - k * per), res, k) for k in range(parts)
+                                          if n - k * per > 0])
+        log(f"{n} synthetic records in {time.perf_counter() - t0:.1f} s")
+        math = args.conv_math if args.dtype == "f32" else "bf16"
+        engines = [Engine(B, res, res, dtype=args.dtype, seed=m, train=False, conv_math=math, tiles=args.tiles)
+                   for m in range(args.members)]
+        evaluate.predict_all(engines, d, B)          # warm-up pass (decoder threads, tiles, caches)
+        t0 = time.perf_counter()
+        preds, labels, _ = evaluate.predict_all(engines, d, B)
+        t_all = time.perf_counter() - t0
+        assert preds[0].shape[0] == n and labels.shape[0] == n
+        ds = lib.dataset.initialize_dataset(d, B, num_workers=evaluate.NUM_WORKERS, prefetch_buffer_size=2 * B,
+                                            image_dim=[res, res], decode_dtype="uint8")
+        t0 = time.perf_counter()
+        it = iter(ds)
+        batches = [b for b in it]
+        lib.dataset.close_iterator(it)
+        t_dec = time.perf_counter() - t0
+        x, y = batches[0]
+        for e in engines:
+            e.set_batch(x, y)
+            e.forward()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(len(batches)):
+            for e in engines:
+                e.forward()
+        for e in engines:
+            e.synchronize()
+        t_gpu = time.perf_counter() - t0
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    M = args.members
+    return {
+        "metric": f"ensemble eval images/sec, Inception-v3 {res}^2, {M} members, batch {B} (evaluate.py -lm)",
+        "value": round(n / t_all, 2), "unit": "images/sec", "n_gpus": 1, "steps": 1, "warmup": 1,
+        "ms_per_step": round(t_all / -(-n // B) * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype,
+        "data": f"{n} synthetic fundus-shaped JPEG q=100 TFRecords at {res}x{res} (jr.synth_records), random Keras "
+                f"init per member",
+        "config": {"workload": f"evaluate.predict_all: {M} resident members x {-(-n // B)} batches of {B}, each "
+                               f"batch read + decoded once (native JPEG, {evaluate.NUM_WORKERS} threads) and run "
+                               f"through every member", "model": "inception_v3", "global_batch": B, "seq_len": None,
+                   "parallelism": "dp1", "members": M, "tiles": engines[0].tiles},
+        "member_images_per_s": round(n * M / t_all, 1),
+        "decode_only_images_per_s": round(n / t_dec, 1),
+        "gpu_forward_only_images_per_s": round(n / t_gpu, 1),
+        "bound": "decode" if t_dec > t_gpu else "gpu",
+    }
+
+
 def main():
     args = parse()
+    if args.mode == "ensemble":
+        out = ensemble_bench(args)
+        print(json.dumps(out), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -42,16 +42,6 @@
  *    n*ho*wo*y_c_stride (dy), c_out*kh*kw*c8 (W^T), kh*kw*c_in*c_out (HWIO).
  *    Eight MFMAs per product in the JR_F32_X8 order; outputs (y, dx, dw) are
  *    fp32 exactly as for JR_F32.
- *    JR_F32_X8W (convolution entry points only) = JR_F32_X8 with only the
- *    FILTER pre-split: fp32 activations and gradients as for JR_F32_X8, the
- *    w argument of fwd / bwd_data = the three bf16 HWIO planes of the filter
- *    (jr_conv_weights_x8p* with w_t = NULL; plane stride kh*kw*c_in*c_out).
- *    Results are BITWISE those of JR_F32_X8 with the same tile configuration
- *    (same products, same order); configuration ids and tuned / pinned
- *    entries are JR_F32_X8's (set_config with either dtype sets both), except
- *    that the fp32-MFMA tile ids (>= 14) need the fp32 filter: fwd / bwd_data
- *    fail with JR_ERR_UNSUPPORTED on them.  bwd_filter under JR_F32_X8W is
- *    JR_F32_X8 (no filter operand).
  */
 #ifndef JR_H_
 #define JR_H_
@@ -71,7 +61,7 @@ typedef enum jr_status {
   JR_ERR_WORKSPACE = -4    /* workspace smaller than *_workspace_size      */
 } jr_status;
 
-typedef enum jr_dtype { JR_F32 = 0, JR_BF16 = 1, JR_F32_X8 = 2, JR_F32_X8P = 3, JR_F32_X8W = 4 } jr_dtype;
+typedef enum jr_dtype { JR_F32 = 0, JR_BF16 = 1, JR_F32_X8 = 2, JR_F32_X8P = 3 } jr_dtype;
 
 typedef enum jr_conv_op { JR_CONV_FWD = 0, JR_CONV_BWD_DATA = 1, JR_CONV_BWD_FILTER = 2 } jr_conv_op;
 

@@ -47,15 +47,6 @@ namespace jr {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-
-// ds_read_b64_tr_b16 (as in jr_conv_bf16.hip): lane 4q+p of each 16-lane
-// group passes the address of row q, columns 4p..4p+3 of the group's 4x16
-// block; lane i gets column i.
-__device__ __forceinline__ s16x4 lds_tr(const uint16_t* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4*)(const_cast<uint16_t*>(p)));
-}
 
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {   // v_cvt_pk_bf16_f32 (RNE), a in the low half
   const bf16x2 r = {(__bf16)a, (__bf16)b};
@@ -138,18 +129,8 @@ struct SplitFrag {
 // (conv1, c_in = 3 padded to 4) every lane keeps its own mixed-radix k
 // counter (generic path).  WGRAD's A operand walks pixels along k, so its
 // lanes advance (b, oh, ow) counters.
-//
-// WP (JR_F32_X8W, FWD / DGRAD): the filter operand B arrives as its three
-// exact bf16 planes h, m, l (HWIO, jr_conv_weights_x8p with no W^T), split
-// once per step instead of in every wave of every block: B's LDS image holds
-// the three bf16 planes (FWD: MC [BK][BN] per plane, read by the
-// transposing ds_read_b64_tr_b16; DGRAD: KC [BN][BK] per plane, one
-// ds_read_b128 per plane and 8 k), and only the activation operand A is split
-// in registers.  The MFMAs, their operands' bits and their order are those
-// of the X8 kernel of the same tile: the result is bitwise X8's.
-template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0, bool WP = false>
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0>
 __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
-  static_assert(!WP || (X8 && OP != OP_WGRAD && DBG == 0), "weight planes: X8 FWD / DGRAD only");
   constexpr int WGN = 4 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
@@ -160,15 +141,11 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int HALF = BK / 2;                // k per lane half
   constexpr bool A_KC = (OP != OP_WGRAD);
   constexpr bool B_KC = (OP == OP_DGRAD);
-  constexpr int ASZ = BM * BK, BSZ = BN * BK;  // floats per image (WP: bf16 elements per B plane)
-  // WP: B's KC rows hold BK bf16 = QPW 16 B quads (DGRAD)
-  constexpr int QPW = BK / 8, RPW = 64 / QPW, SWW = 16 / QPW;
-  constexpr int BIMG = WP ? 3 * BSZ / 2 : BSZ;                     // floats of B's LDS image (all planes)
-  constexpr int STG = ASZ + BIMG;                                  // floats per ring slot
-  constexpr int A_INSTR = ASZ / 256, B_INSTR = WP ? BSZ / 512 : BSZ / 256;   // WP: per plane
+  constexpr int ASZ = BM * BK, BSZ = BN * BK;  // floats per image
+  constexpr int A_INSTR = ASZ / 256, B_INSTR = BSZ / 256;
   constexpr int A_PW = (A_INSTR + 3) / 4, B_PW = (B_INSTR + 3) / 4;  // per wave
-  static_assert(ASZ % 256 == 0 && BSZ % (WP ? 512 : 256) == 0, "tile must be whole DMA instructions");
-  constexpr int SMEM = NBUF * STG > 4 * stage_floats<WN>() ? NBUF * STG : 4 * stage_floats<WN>();
+  static_assert(ASZ % 256 == 0 && BSZ % 256 == 0, "tile must be whole DMA instructions");
+  constexpr int SMEM = NBUF * (ASZ + BSZ) > 4 * stage_floats<WN>() ? NBUF * (ASZ + BSZ) : 4 * stage_floats<WN>();
   __shared__ __attribute__((aligned(1024))) float smem[SMEM];
   JR_ST(Stamps stamp; stamp.start();)
 
@@ -279,34 +256,14 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   }
   // ---------------------------------------------------------------- B state
   const float* b_ptr[B_PW];
-  const uint16_t* bw_ptr[B_PW];             // WP: the h plane of the piece's source
   int b_p0[B_PW], b_s0[B_PW], b_s1[B_PW], b_s2[B_PW];
-  const uint16_t* gBw = reinterpret_cast<const uint16_t*>(g.B);
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
     const int j = wave + 4 * i;
     b_ptr[i] = zp;
-    bw_ptr[i] = reinterpret_cast<const uint16_t*>(zp);
     b_p0[i] = b_s0[i] = b_s1[i] = b_s2[i] = 0;
     if (B_INSTR % 4 != 0 && j >= B_INSTR) continue;
-    if constexpr (WP && B_KC) {  // DGRAD planes: rows = ci, k = (a, bb, co), 8 bf16 per quad
-      const int row = j * RPW + lane / QPW;
-      const int q = (lane % QPW) ^ ((row / SWW) % QPW);
-      const int nn = n0 + row;
-      b_p0[i] = nn < g.N ? nn : -1;
-      bw_ptr[i] = gBw + ((long long)(nn < g.N ? nn : 0) * g.cout + (ut ? q * 8 : 0));
-      const int k = kt0 * BK + q * 8;
-      const int ab = k / g.cout;
-      b_s2[i] = k - ab * g.cout;
-      b_s0[i] = ab / g.nb;
-      b_s1[i] = ab - b_s0[i] * g.nb;
-    } else if constexpr (WP) {   // FWD planes, MC [BK][BN]: 8 bf16 columns per piece
-      const int flat = j * 512 + lane * 8;
-      const int krow = flat / BN, col = flat - krow * BN;
-      b_p0[i] = (n0 + col < g.N) ? n0 + col : -1;
-      b_s0[i] = kt0 * BK + krow;
-      bw_ptr[i] = gBw + ((long long)b_s0[i] * g.N + (n0 + col));
-    } else if constexpr (B_KC) {  // DGRAD: rows = ci, k = (a, bb, co)
+    if constexpr (B_KC) {  // DGRAD: rows = ci, k = (a, bb, co)
       const int row = j * RPI + lane / QPR;
       const int q = (lane % QPR) ^ ((row / SWZ) % QPR);
       const int nn = n0 + row;
@@ -403,36 +360,6 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     const int i = d - A_PW;
     const int j = wave + 4 * i;
     if (B_INSTR % 4 != 0 && j >= B_INSTR) return;
-    if constexpr (WP) {   // one piece = the same 16 B of each of the three planes
-      const uint16_t* zpw = reinterpret_cast<const uint16_t*>(zp);
-      uint16_t* dst = reinterpret_cast<uint16_t*>(Bs) + j * 512;
-      bool ok;
-      const uint16_t* src;
-      if constexpr (B_KC) {   // DGRAD: W[(r0+sh*a, c0+sw*bb)][ci][co]
-        if constexpr (ut) {
-          const long long off = (long long)((g.r0 + g.sh * t_r) * g.kw + (g.c0 + g.sw * t_c)) * g.cin * g.cout + t_ch;
-          ok = b_p0[i] >= 0;
-          src = bw_ptr[i] + off;
-        } else {
-          ok = (b_p0[i] >= 0) & (b_s0[i] < g.na);
-          const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
-          src = gBw + (((long long)(r * g.kw + c) * g.cin + (b_p0[i] >= 0 ? b_p0[i] : 0)) * g.cout + b_s2[i]);
-          adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
-        }
-      } else {                // FWD: W[k][n], MC
-        const int k = b_s0[i] + (kt - kt0) * BK;
-        ok = (b_p0[i] >= 0) & (k < g.K);
-        src = bw_ptr[i] + (long long)(kt - kt0) * BK * g.N;
-        if (!ut && g.cp != g.cin) {   // virtual channel padding (conv1): uniform branch
-          const int rc = k / g.cp, ci = k - rc * g.cp;
-          ok = ok & (ci < g.cin);
-          src = gBw + ((long long)(rc * g.cin + ci) * g.N + (b_p0[i] >= 0 ? b_p0[i] : 0));
-        }
-      }
-#pragma unroll
-      for (int p = 0; p < 3; ++p) dma16(ok ? src + p * g.b_ps : zpw, dst + p * BSZ);
-      return;
-    }
     if constexpr (B_KC) {  // DGRAD: W[(r0+sh*a, c0+sw*bb)][ci][co]
       if constexpr (ut) {
         const long long off = (long long)((g.r0 + g.sh * t_r) * g.kw + (g.c0 + g.sw * t_c)) * g.cin * g.cout + t_ch;
@@ -493,7 +420,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   // issues one more piece per tile (A_INSTR or B_INSTR not a multiple of 4)
   // then waits for one piece of a newer tile too — safe, and it keeps the
   // K loop free of per-wave branches.
-  constexpr int per_tile = A_INSTR / 4 + (WP ? 3 : 1) * (B_INSTR / 4);
+  constexpr int per_tile = A_INSTR / 4 + B_INSTR / 4;
 
   // One K-tile: fragments of tile kt (LDS -> VGPRs), then MFMAs from
   // registers with the DMA of tile kt+NBUF-1 (into the buffer read in
@@ -505,19 +432,8 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   auto step = [&](int kt, auto do_issue, const float* __restrict__ As, const float* __restrict__ Bs,
                   float* __restrict__ wA, float* __restrict__ wB) {
     constexpr bool DO_ISSUE = decltype(do_issue)::value;
-    float af[TM][HALF], bfr[TN][WP ? 1 : HALF];
-    if constexpr (WP) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm0 + i * 32 + l31;
-        const int f = (row / SWZ) % QPR;
-#pragma unroll
-        for (int t = 0; t < QPR / 2; ++t) {
-          const float4 v = *reinterpret_cast<const float4*>(As + row * BK + (((lh * (QPR / 2) + t) ^ f) * 4));
-          af[i][4 * t + 0] = v.x; af[i][4 * t + 1] = v.y; af[i][4 * t + 2] = v.z; af[i][4 * t + 3] = v.w;
-        }
-      }
-    } else if constexpr (DBG == 3) {
+    float af[TM][HALF], bfr[TN][HALF];
+    if constexpr (DBG == 3) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -592,80 +508,6 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc[i][j], 0, 0, 0);
         }
       };
-      if constexpr (WP) {
-        // B's planes from LDS: lane (l31, lh) takes column / row l31 of the
-        // fragment and k = lh * HALF + 8 g8 + 0..7, as the X8 fragment
-        const uint16_t* Bw = reinterpret_cast<const uint16_t*>(Bs);
-        const int hb = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
-#pragma unroll
-        for (int g8 = 0; g8 < G8; ++g8) {
-          bf16x8 bh[TN], bm[TN], bl[TN];
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            bf16x8 v[3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p) {
-              if constexpr (B_KC) {
-                const int row = wn0 + j * 32 + l31;
-                const int f = (row / SWW) % QPW;
-                v[p] = *reinterpret_cast<const bf16x8*>(Bw + p * BSZ + row * BK + (((lh * (HALF / 8) + g8) ^ f) * 8));
-              } else {
-                const uint16_t* q = Bw + p * BSZ + (lh * HALF + 8 * g8 + tq) * BN + wn0 + j * 32 + 16 * hb + 4 * tp;
-                const s16x4 lo = lds_tr(q), hi = lds_tr(q + 4 * BN);
-                v[p] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-              }
-            }
-            bh[j] = v[0]; bm[j] = v[1]; bl[j] = v[2];
-          }
-          SplitFrag sa[TM];
-#pragma unroll
-          for (int i = 0; i < TM; ++i) sa[i].init(&af[i][8 * g8], false);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) mma(i, j, sa[i].h(), bh[j]);
-#pragma unroll
-          for (int i = 0; i < TM; ++i) sa[i].stage2(false);
-          next_piece();
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) mma(i, j, sa[i].m(), bh[j]);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              mma(i, j, sa[i].h(), bm[j]);
-              mma(i, j, sa[i].m(), bm[j]);
-            }
-#pragma unroll
-          for (int i = 0; i < TM; ++i) sa[i].stage3(false);
-          next_piece();
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) mma(i, j, sa[i].l(), bh[j]);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              mma(i, j, sa[i].h(), bl[j]);
-              if constexpr (kSplitTerms == 8) {
-                mma(i, j, sa[i].m(), bl[j]);
-                mma(i, j, sa[i].l(), bm[j]);
-              }
-            }
-          next_piece();
-        }
-        if constexpr (DO_ISSUE) {
-#pragma unroll
-          for (int d = 3 * G8; d < NPIECE; ++d) issue_piece(kt + NBUF - 1, d, wA, wB);
-          advance();
-        }
-        return;
-      }
 #pragma unroll
       for (int g8 = 0; g8 < G8; ++g8) {
         SplitFrag sa[TM], sb[TN];
@@ -752,7 +594,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     // prologue: tiles kt0 .. kt0+NBUF-2 in flight
 #pragma unroll
     for (int p = 0; p < NBUF - 1; ++p)
-      if (kt0 + p < kt1) issue(kt0 + p, smem + p * STG, smem + p * STG + ASZ);
+      if (kt0 + p < kt1) issue(kt0 + p, smem + p * (ASZ + BSZ), smem + p * (ASZ + BSZ) + ASZ);
     wait_vmcnt(per_tile * min(NBUF - 2, kt1 - kt0 - 1));
     __builtin_amdgcn_s_barrier();
     JR_ST(stamp.prologue();)
@@ -762,8 +604,8 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     // tile kt+1 landed once at most (NBUF-2) tiles per wave are outstanding
     for (; kt < kt1 - (NBUF - 1); ++kt) {
       const int nxt = cur == 0 ? NBUF - 1 : cur - 1;
-      step(kt, std::true_type{}, smem + cur * STG, smem + cur * STG + ASZ,
-           smem + nxt * STG, smem + nxt * STG + ASZ);
+      step(kt, std::true_type{}, smem + cur * (ASZ + BSZ), smem + cur * (ASZ + BSZ) + ASZ,
+           smem + nxt * (ASZ + BSZ), smem + nxt * (ASZ + BSZ) + ASZ);
       // sched_barrier keeps hipcc from sinking the register-only MFMAs below
       // the wait; one barrier: every wave's part of tile kt+1 is in LDS and
       // every wave is done reading tile kt
@@ -777,7 +619,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     }
     // drain: no more DMA to issue
     for (; kt < kt1; ++kt) {
-      step(kt, std::false_type{}, smem + cur * STG, smem + cur * STG + ASZ, nullptr, nullptr);
+      step(kt, std::false_type{}, smem + cur * (ASZ + BSZ), smem + cur * (ASZ + BSZ) + ASZ, nullptr, nullptr);
       __builtin_amdgcn_sched_barrier(0);
       JR_ST(const unsigned long long tw = stamp.now();)
       wait_vmcnt(per_tile * max(0, min(NBUF - 2, kt1 - kt - 2)));
@@ -819,9 +661,6 @@ struct Plan {
 // Channel padding of the reduction operand: 16 B DMA pieces hold 4 fp32 or
 // 8 bf16 channels.
 static bool bf16_operands(int dtype) { return dtype == JR_BF16 || dtype == JR_F32_X8P; }
-// JR_F32_X8W is JR_F32_X8 with the filter operand as three bf16 planes: the
-// same kernels, tiles, configuration ids and tuned / pinned entries
-static bool is_x8(int dtype) { return dtype == JR_F32_X8 || dtype == JR_F32_X8W; }
 static int chan_pad(int c, int dtype) {
   const int q = bf16_operands(dtype) ? 8 : 4;
   return (c + q - 1) / q * q;
@@ -845,13 +684,13 @@ static int wide_base(int dtype) {
 static int cfg_count(int dtype) {
   return dtype == JR_BF16 ? wide_base(dtype) + kNumCfgsBf16W
          : dtype == JR_F32_X8P ? wide_base(dtype) + kNumCfgsX8PW
-         : std_count(dtype) + (is_x8(dtype) ? kNumCfgs : 0);
+         : std_count(dtype) + (dtype == JR_F32_X8 ? kNumCfgs : 0);
 }
 static bool is_halo(int dtype, int tile) {
   return dtype == JR_BF16 && tile >= kNumCfgsBf16 && tile < kNumCfgsBf16 + kNumHaloBf16;
 }
 static bool is_wide(int dtype, int tile) { return tile >= wide_base(dtype) && tile < cfg_count(dtype); }
-static bool is_x8_f32(int dtype, int tile) { return is_x8(dtype) && tile >= kNumCfgs; }
+static bool is_x8_f32(int dtype, int tile) { return dtype == JR_F32_X8 && tile >= kNumCfgs; }
 static const TileCfg& tile_cfg(int dtype, int tile) {
   if (is_halo(dtype, tile)) return kHaloBf16[tile - kNumCfgsBf16].t;
   if (is_wide(dtype, tile)) return (dtype == JR_BF16 ? kCfgsBf16W : kCfgsX8PW)[tile - wide_base(dtype)];
@@ -941,8 +780,7 @@ static void tune_set(const TuneKey& k, int cfg) {   // g_tune_mu held; cfg < 0 e
 }
 
 static TuneKey tune_key(int dtype, int op, int M, int N, int K, const jr_conv_desc* d) {
-  return TuneKey{is_x8(dtype) ? (int)JR_F32_X8 : dtype, op, M, N, K, d->h, d->w, d->kh, d->kw, d->stride_h, d->c_in,
-                 d->c_out, d->n};
+  return TuneKey{dtype, op, M, N, K, d->h, d->w, d->kh, d->kw, d->stride_h, d->c_in, d->c_out, d->n};
 }
 
 static Plan make_plan(int dtype, int op, int M, int N, int K, const jr_conv_desc* d, int force_cfg = -1) {
@@ -1011,41 +849,40 @@ static size_t stats_ws(int dtype, const Plan& p) {
 // Fast-path kernels (UT): FWD/DGRAD when the reduction channel radix is a
 // multiple of BK (every layer but conv1 FWD at BK = 16); WGRAD when BK / wo < ho
 // (one carry per radix and K-tile: the incremental pixel walk).
-template <int OP, int C, int DBG, bool X8, bool WP>
+template <int OP, int C, int DBG, bool X8>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t s) {
   constexpr TileCfg t = kCfgs[C];
   const bool fast = OP == OP_WGRAD ? t.bk / a.wo < a.ho : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
   if (fast) {
-    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, X8, DBG, WP>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, X8, DBG>), grid, dim3(256), 0, s, a);
     return;
   }
   if constexpr (DBG == 0)
-    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, X8, 0, WP>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, X8, 0>), grid, dim3(256), 0, s, a);
 }
 
-// WP (JR_F32_X8W): the X8 kernel with the filter operand as bf16 planes
-template <int OP, int DBG = 0, bool X8 = false, bool WP = false>
+template <int OP, int DBG = 0, bool X8 = false>
 static void launch_op(int cfg, const ConvArgs& a, dim3 grid, hipStream_t s) {
   switch (cfg) {
-    case 0: launch_cfg<OP, 0, DBG, X8, WP>(a, grid, s); break;
-    case 1: launch_cfg<OP, 1, DBG, X8, WP>(a, grid, s); break;
-    case 2: launch_cfg<OP, 2, DBG, X8, WP>(a, grid, s); break;
-    case 3: launch_cfg<OP, 3, DBG, X8, WP>(a, grid, s); break;
-    case 4: launch_cfg<OP, 4, DBG, X8, WP>(a, grid, s); break;
-    case 5: launch_cfg<OP, 5, DBG, X8, WP>(a, grid, s); break;
-    case 6: launch_cfg<OP, 6, DBG, X8, WP>(a, grid, s); break;
-    case 7: launch_cfg<OP, 7, DBG, X8, WP>(a, grid, s); break;
-    case 8: launch_cfg<OP, 8, DBG, X8, WP>(a, grid, s); break;
-    case 9: launch_cfg<OP, 9, DBG, X8, WP>(a, grid, s); break;
-    case 10: launch_cfg<OP, 10, DBG, X8, WP>(a, grid, s); break;
-    case 11: launch_cfg<OP, 11, DBG, X8, WP>(a, grid, s); break;
-    case 12: launch_cfg<OP, 12, DBG, X8, WP>(a, grid, s); break;
-    default: launch_cfg<OP, 13, DBG, X8, WP>(a, grid, s); break;
+    case 0: launch_cfg<OP, 0, DBG, X8>(a, grid, s); break;
+    case 1: launch_cfg<OP, 1, DBG, X8>(a, grid, s); break;
+    case 2: launch_cfg<OP, 2, DBG, X8>(a, grid, s); break;
+    case 3: launch_cfg<OP, 3, DBG, X8>(a, grid, s); break;
+    case 4: launch_cfg<OP, 4, DBG, X8>(a, grid, s); break;
+    case 5: launch_cfg<OP, 5, DBG, X8>(a, grid, s); break;
+    case 6: launch_cfg<OP, 6, DBG, X8>(a, grid, s); break;
+    case 7: launch_cfg<OP, 7, DBG, X8>(a, grid, s); break;
+    case 8: launch_cfg<OP, 8, DBG, X8>(a, grid, s); break;
+    case 9: launch_cfg<OP, 9, DBG, X8>(a, grid, s); break;
+    case 10: launch_cfg<OP, 10, DBG, X8>(a, grid, s); break;
+    case 11: launch_cfg<OP, 11, DBG, X8>(a, grid, s); break;
+    case 12: launch_cfg<OP, 12, DBG, X8>(a, grid, s); break;
+    default: launch_cfg<OP, 13, DBG, X8>(a, grid, s); break;
   }
 }
 
 static int validate(const jr_conv_desc* d, int op, int dtype) {
-  if (dtype != JR_F32 && dtype != JR_BF16 && dtype != JR_F32_X8 && dtype != JR_F32_X8P && dtype != JR_F32_X8W)
+  if (dtype != JR_F32 && dtype != JR_BF16 && dtype != JR_F32_X8 && dtype != JR_F32_X8P)
     return fail(JR_ERR_INVALID, "conv: bad dtype");
   const int q = bf16_operands(dtype) ? 8 : 4;   // channels per 16 B piece
   if (!d) return fail(JR_ERR_INVALID, "conv: null descriptor");
@@ -1148,12 +985,8 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     else
       launch_conv_bf16(OP, p.tile, am, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
   } else if (is_x8_f32(dtype, p.tile)) {
-    if (dtype == JR_F32_X8W && OP != OP_WGRAD)
-      return fail(JR_ERR_UNSUPPORTED, "conv JR_F32_X8W: an fp32-MFMA tile needs the fp32 filter (use JR_F32_X8)");
     launch_op<OP>(p.tile - kNumCfgs, a, grid, s);     // the fp32-MFMA kernel of that tile
-  } else if (dtype == JR_F32_X8W && OP != OP_WGRAD) {
-    if constexpr (OP != OP_WGRAD) launch_op<OP, 0, true, true>(p.tile, a, grid, s);  // filter = its three bf16 planes
-  } else if (is_x8(dtype)) {
+  } else if (dtype == JR_F32_X8) {
     launch_op<OP, 0, true>(p.tile, a, grid, s);
   } else {
     launch_op<OP>(p.tile, a, grid, s);
@@ -1274,8 +1107,6 @@ static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, con
     else if (op == OP_DGRAD) { a.a_ps = ye; a.b_ps = we; }
     else { a.a_ps = xe; a.b_ps = ye; }
   }
-  if (dtype == JR_F32_X8W)   // filter planes: HWIO, plane stride = the filter's element count
-    a.b_ps = (long long)d->kh * d->kw * d->c_in * d->c_out;
   hipStream_t s = as_stream(stream);
   void* out = C;
   if (op == OP_FWD) {
@@ -1328,7 +1159,6 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
     float best_t = 1e30f;
     auto time_cfg = [&](int c) -> float {
       if (is_halo(dtype, cfg_tile(c)) && !halo_ok(d, op, dtype, cfg_tile(c))) return 1e30f;
-      if (dtype == JR_F32_X8W && op != OP_WGRAD && is_x8_f32(dtype, cfg_tile(c))) return 1e30f;   // needs fp32 w
       const Plan pc = plan_with(dtype, c, M, N, K);
       // FWD runs with the fused BN statistics: their partials must fit too
       if ((op == OP_FWD ? align256(plan_ws(pc)) + stats_ws(dtype, pc) : plan_ws(pc)) > ws_bytes) return 1e30f;
@@ -1579,7 +1409,7 @@ JR_API int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const vo
 }
 
 JR_API int jr_conv2d_num_configs(int dtype) {
-  return dtype == JR_BF16 || dtype == JR_F32 || is_x8(dtype) || dtype == JR_F32_X8P ? cfg_count(dtype) : 0;
+  return dtype == JR_BF16 || dtype == JR_F32 || dtype == JR_F32_X8 || dtype == JR_F32_X8P ? cfg_count(dtype) : 0;
 }
 
 // Diagnostic: time `reps` launches of one FWD GEMM (no split-K) of tile

@@ -102,8 +102,7 @@ def predict_all(engines, data_dir, batch_size, rank=0, world=1):
     """Per-member predictions over this rank's batches: ([M][n_r, 1], [n_r, 1],
     batch indices).  Each batch is decoded once (this rank's batches only)
     and run through every member."""
-    from jr.session import Session
-    sessions = [Session(e) for e in engines]
+    import torch
     dataset = lib.dataset.initialize_dataset(
         data_dir, batch_size, num_workers=NUM_WORKERS, prefetch_buffer_size=2 * batch_size,
         image_data_format="channels_last", num_channels=NUM_CHANNELS,
@@ -116,10 +115,18 @@ def predict_all(engines, data_dir, batch_size, rank=0, world=1):
         for k, (x, y) in enumerate(it):
             ids.append(k * world + rank)
             got_y.append(y)
-            for m, sess in enumerate(sessions):
-                out = lib.evaluation.perform_test(sess=sess, init_op=None, feed_dict_fn=_one_batch(x, y),
-                                                  custom_tensors=["predictions"])
-                preds[m].append(out[0])
+            # every member's forward is enqueued before the first result is
+            # read back (one host sync per batch, not per member), while the
+            # decoder threads already work on the next batches
+            # (the uint8 batch crosses PCIe once for all members)
+            xd = torch.as_tensor(x).to(engines[0].device)
+            torch.cuda.current_stream(engines[0].device).synchronize()
+            n = 0
+            for e in engines:
+                n = e.set_batch(xd, y)
+                e.forward(n)
+            for m, e in enumerate(engines):
+                preds[m].append(e.predictions(n))
     finally:
         lib.dataset.close_iterator(it)
     empty = np.zeros((0, 1), np.float32)

@@ -19,7 +19,6 @@ JR_F32 = 0
 JR_BF16 = 1
 JR_F32_X8 = 2      # conv entry points only: fp32 tensors, bf16x8-split MFMA products (jr.h)
 JR_F32_X8P = 3     # conv entry points only: the X8 arithmetic on pre-split h/m/l bf16 operand planes (jr.h)
-JR_F32_X8W = 4     # conv entry points only: X8 with the filter operand as its h/m/l bf16 HWIO planes (jr.h)
 JR_CONV_FWD, JR_CONV_BWD_DATA, JR_CONV_BWD_FILTER = 0, 1, 2
 JR_HEAD_SIGMOID, JR_HEAD_SOFTMAX = 0, 1
 

@@ -88,11 +88,6 @@ class Engine:
         self.conv_math = conv_math
         self.x8p = conv_math == "x8p"
         self.cdt = {"x8": _ffi.JR_F32_X8, "x8p": _ffi.JR_F32_X8P}.get(conv_math, self.dt)
-        # x8: the forward and data-gradient GEMMs take the filter as its three
-        # exact bf16 planes (JR_F32_X8W, split once per step by the weight
-        # prep instead of in every wave): bitwise the JR_F32_X8 result, same
-        # tile configs (JR_X8W=0 turns it off, for A/B runs)
-        self.x8w = conv_math == "x8" and os.environ.get("JR_X8W", "1") != "0"
         self.train_mode = train
         if optimizer not in ("nesterov", "momentum", "sgd", "adam"):
             raise ValueError(f"unknown optimizer {optimizer}")
@@ -214,8 +209,6 @@ class Engine:
             self.dfeat = self._t(B * feat_c)
         if self.dt == _ffi.JR_BF16 or self.x8p:
             self._alloc_bf16_filters(planes=3 if self.x8p else 1)
-        elif self.x8w:
-            self._alloc_bf16_filters(planes=3, transposed=False)
         if self.x8p:
             self._alloc_planes()
         ws = 0
@@ -250,13 +243,12 @@ class Engine:
             n = max(B * u.ho * u.wo * u.cout for u in self.cunits)
             self.drawp_lane = [self._t(3 * n, bf) for _ in range(self.nlanes)]
 
-    def _alloc_bf16_filters(self, planes: int = 1, transposed: bool = True) -> None:
+    def _alloc_bf16_filters(self, planes: int = 1) -> None:
         """bf16 operand copies of every conv launch's kernel (block), refreshed
         from the fp32 master parameters by ONE jr_conv_weights_bf16_multi
         launch at the start of each forward: HWIO (bwd_data) and
         W^T [co][kh][kw][c8] (fwd).  planes = 3 (JR_F32_X8P): each copy is
-        the three bf16 planes of the exact split, jr_conv_weights_x8p_multi.
-        transposed = False (JR_F32_X8W): the HWIO planes only."""
+        the three bf16 planes of the exact split, jr_conv_weights_x8p_multi."""
         L = self.lib
         self.wplanes = planes
         layers, tiles = [], 0
@@ -271,45 +263,24 @@ class Engine:
             # stride = the layer's element count (jr.h)
             hw_n = u.kh * u.kw * u.cin * u.cout
             ho += (planes * hw_n + 7) // 8 * 8
-            if transposed:
-                to += planes * u.cout * u.kh * u.kw * c8
+            to += planes * u.cout * u.kh * u.kw * c8
         arr = (_ffi.WPrep * len(layers))(*layers)
         self.wprep_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
         self.wprep_layers, self.wprep_tiles = len(layers), tiles
         self.w_hwio = self._t(ho, torch.bfloat16)
-        self.w_t = self._t(to, torch.bfloat16) if transposed else None
+        self.w_t = self._t(to, torch.bfloat16)
 
     def _wprep_call(self, stream=None):
         fn = self.lib.jr_conv_weights_x8p_multi if self.wplanes == 3 else self.lib.jr_conv_weights_bf16_multi
         return (fn,
                 (self.wprep_table.data_ptr(), self.wprep_layers, self.wprep_tiles, self.params.data_ptr(),
-                 self.w_hwio.data_ptr(), self.w_t.data_ptr() if self.w_t is not None else None, stream or self._s),
-                "wprep_bf16")
+                 self.w_hwio.data_ptr(), self.w_t.data_ptr(), stream or self._s), "wprep_bf16")
 
     def _wf(self, u: ConvUnit) -> int:
         """Filter operand of conv fwd: fp32 HWIO master block, or its bf16 W^T copy (planes)."""
         if self.dt == _ffi.JR_BF16 or self.x8p:
             return self.w_t.data_ptr() + 2 * self.wb_t_off[u.first.idx]
         return self.params.data_ptr() + 4 * u.koff
-
-    def _fwd_w(self, u: ConvUnit):
-        """(conv dtype code, filter operand) of the unit's forward: JR_F32_X8W
-        on the HWIO planes unless its tile is an fp32-MFMA one (ids >= 14)."""
-        if self.x8w and self.lib.jr_conv2d_get_config(ctypes.byref(self._conv_desc(u, self.batch)),
-                                                      _ffi.JR_CONV_FWD, self.cdt, 0) & 255 < 14:
-            return _ffi.JR_F32_X8W, self.w_hwio.data_ptr() + 2 * self.wb_hwio_off[u.first.idx]
-        return self.cdt, self._wf(u)
-
-    def _dgrad_w(self, u: ConvUnit):
-        """(conv dtype code, filter operand) of the unit's data gradient (every
-        stride phase's tile must take the planes for JR_F32_X8W)."""
-        if self.x8w:
-            d = self._conv_desc(u, self.batch)
-            cf = [self.lib.jr_conv2d_get_config(ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.cdt, p)
-                  for p in range(u.stride * u.stride)]
-            if all(c & 255 < 14 for c in cf):
-                return _ffi.JR_F32_X8W, self.w_hwio.data_ptr() + 2 * self.wb_hwio_off[u.first.idx]
-        return self.cdt, self._wd(u)
 
     def _wd(self, u: ConvUnit) -> int:
         """Filter operand of conv bwd_data: fp32 HWIO master block, or its bf16 copy (planes)."""
@@ -326,15 +297,9 @@ class Engine:
         self._drop_calls()
         ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
         s = self._s
-        if self.dt == _ffi.JR_BF16 or self.x8p or self.x8w:
+        if self.dt == _ffi.JR_BF16 or self.x8p:
             fn, args, name = self._wprep_call()
             _ffi.check(name, fn(*args))
-        # x8w: the forward / data-gradient GEMMs are timed in the kernel they run
-        # (JR_F32_X8W: fp32-MFMA tiles fail there and drop out of the race)
-        wf = (lambda u: (_ffi.JR_F32_X8W, self.w_hwio.data_ptr() + 2 * self.wb_hwio_off[u.first.idx])) \
-            if self.x8w else (lambda u: (self.cdt, self._wf(u)))  # noqa: E731
-        wd = (lambda u: (_ffi.JR_F32_X8W, self.w_hwio.data_ptr() + 2 * self.wb_hwio_off[u.first.idx])) \
-            if self.x8w else (lambda u: (self.cdt, self._wd(u)))  # noqa: E731
         for u in self.cunits:
             if progress is not None:
                 progress(u.name)
@@ -342,8 +307,8 @@ class Engine:
             x = (self.aplanes[u.x] if self.x8p else self.acts[u.x]).data_ptr()
             draw = (self.drawp_lane[0] if self.x8p else self.draw).data_ptr() if self.train_mode else 0
             raw = self.raw_unit[u.first.idx].data_ptr()
-            _ffi.check("autotune fwd", L.jr_conv2d_autotune(ctypes.byref(d), _ffi.JR_CONV_FWD, wf(u)[0], x,
-                                                             wf(u)[1], raw, ws, wsb, s))
+            _ffi.check("autotune fwd", L.jr_conv2d_autotune(ctypes.byref(d), _ffi.JR_CONV_FWD, self.cdt, x,
+                                                             self._wf(u), raw, ws, wsb, s))
             if not self.train_mode:
                 continue
             _ffi.check("autotune wgrad", L.jr_conv2d_autotune(
@@ -351,7 +316,7 @@ class Engine:
                 self.grads.data_ptr() + 4 * u.koff, ws, wsb, s))
             if u.x != self.g.input_buf:
                 _ffi.check("autotune dgrad", L.jr_conv2d_autotune(
-                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, wd(u)[0], draw, wd(u)[1],
+                    ctypes.byref(d), _ffi.JR_CONV_BWD_DATA, self.cdt, draw, self._wd(u),
                     self.dacts[u.x].data_ptr(), ws, wsb, s))
         self.synchronize()
         if self.train_mode:
@@ -546,7 +511,7 @@ class Engine:
         unit_of = self.plan.unit_of
         x8p = self.x8p
         wkey = ("w16",) if (dt == _ffi.JR_BF16 or x8p) else ("p",)
-        if dt == _ffi.JR_BF16 or x8p or self.x8w:
+        if dt == _ffi.JR_BF16 or x8p:
             add(fwd, *self._wprep_call(S[0]), 0, [("p",)], [("w16",)])
         # x8p: conv operands are the split planes of the input buffer, written
         # once (by the lane of its first consumer) when the buffer is complete
@@ -575,12 +540,10 @@ class Engine:
                                               self.batch * b.h * b.w * cp, s),
                         "split_x8p", ln, a_all(u.x), [("ap", u.x)], nbytes=rows * (4 * b.c + 6 * cp))
                 # conv + the BN batch statistics of its raw output, fused
-                fdt, fw = self._fwd_w(u)
-                add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), fdt, AX(u.x), fw, raw, BN_EPS,
+                add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), cdt, AX(u.x), self._wf(u), raw, BN_EPS,
                                                     self.mean_unit[uid].data_ptr(),
                                                     self.invstd_unit[uid].data_ptr(), ws, wsb, s),
-                    "conv_fwd", ln, ax_reads(u.x) + [("w16",) if fdt == _ffi.JR_F32_X8W else wkey],
-                    [("r", uid), ("ws", ln)])
+                    "conv_fwd", ln, ax_reads(u.x) + [wkey], [("r", uid), ("ws", ln)])
                 for m, co in zip(u.members, u.col_off):
                     yb = g.bufs[m.y.buf]
                     add(fwd, L.jr_bn_relu_apply, (dt, raw, co, u.cout, M, m.cout, self.mean[m.idx].data_ptr(),
@@ -703,10 +666,9 @@ class Engine:
                                                           self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
                             "conv_wgrad", ln, ax_reads(u.x) + [dkey], [("g", uid), ("ws", ln)])
                     if u.x != g.input_buf:
-                        ddt, dw_ = self._dgrad_w(u) if not x8p else (cdt, self._wd(u))
-                        add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), ddt, draw, dw_, D(u.x), acc, ws, wsb, s),
-                            "conv_dgrad", ln, [dkey, ("w16",) if ddt == _ffi.JR_F32_X8W else wkey],
-                            d_all(u.x) + [("ws", ln)])
+                        add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), cdt, draw, self._wd(u), D(u.x), acc, ws, wsb,
+                                                        s),
+                            "conv_dgrad", ln, [dkey, wkey], d_all(u.x) + [("ws", ln)])
                         written.add(u.x)
                     trigger = False
                     while flush_at and flush_at[0] >= u.koff:

@@ -1,6 +1,6 @@
 """Diagnostic: is the x8 conv GEMM bound by power (operand bit activity)?
-Times one conv5 forward GEMM (64 x 73^2 x 80 -> 192, 3x3; pinned tile) under
-JR_F32_X8 and JR_F32_X8W on (a) random fp32 operands, (b) operands that are
+Times conv forward GEMMs (conv5 64 x 73^2 x 80 -> 192 3x3, a 17^2 1x7 and
+a 35^2 1x1; tile `cfg`, one split) under JR_F32_X8 on (a) random fp32 operands, (b) operands that are
 exactly bf16 (the m / l split terms are zero), (c) zeros -- ~1 s of
 back-to-back launches each, then 50 timed.
   python tools/x8_power_probe.py [cfg]"""
@@ -35,10 +35,8 @@ for name, (n, h, w, ci, co, kh, kw, pw) in cases.items():
     data = {"random": (xr, wr), "bf16-exact": (xr.bfloat16().float(), wr.bfloat16().float()),
             "zeros": (torch.zeros_like(xr), torch.zeros_like(wr))}
     for kind, (x, wt) in data.items():
-        hw = torch.zeros(3 * wt.numel(), dtype=torch.bfloat16, device="cuda")
-        _ffi.check("wprep", L.jr_conv_weights_x8p(wt.data_ptr(), kh, kw, ci, co, hw.data_ptr(), None, None))
         res = []
-        for dt, wp in ((_ffi.JR_F32_X8, wt), (_ffi.JR_F32_X8W, hw)):
+        for dt, wp in ((_ffi.JR_F32_X8, wt),):
             def run():
                 _ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), dt, x.data_ptr(), wp.data_ptr(), y.data_ptr(),
                                                   ws.data_ptr(), wsb, None))
@@ -54,6 +52,6 @@ for name, (n, h, w, ci, co, kh, kw, pw) in cases.items():
             e1.record()
             torch.cuda.synchronize()
             t = e0.elapsed_time(e1) / 50 / 1e3
-            res.append(f"{'x8w' if dt == _ffi.JR_F32_X8W else 'x8 '} {t * 1e6:7.1f} us {flops / t / 1e12:6.1f} TF/s")
+            res.append(f"x8 {t * 1e6:7.1f} us {flops / t / 1e12:6.1f} TF/s")
         print(f"{name:24s} cfg {cfg:2d} {kind:10s}: " + " | ".join(res), flush=True)
     _ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, _ffi.JR_F32_X8, 0, -1))
