@@ -56,6 +56,8 @@ def parse():
                          "(TFRecord read + JPEG decode + every member's forward) over synthetic records")
     ap.add_argument("--members", type=int, default=10, help="ensemble mode: members resident on the GPU")
     ap.add_argument("--images", type=int, default=2048, help="ensemble mode: synthetic test images")
+    ap.add_argument("--per-member", action="store_true",
+                    help="ensemble mode: one engine per member instead of the grouped EnsembleEngine")
     ap.add_argument("--res", type=int, default=299)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--conv-math", default="x8", choices=["f32", "x8", "x8p"],
@@ -266,8 +268,16 @@ def ensemble_bench(args) -> dict:
                                           if n - k * per > 0])
         log(f"{n} synthetic records in {time.perf_counter() - t0:.1f} s")
         math = args.conv_math if args.dtype == "f32" else "bf16"
-        engines = [Engine(B, res, res, dtype=args.dtype, seed=m, train=False, conv_math=math, tiles=args.tiles)
-                   for m in range(args.members)]
+        if args.per_member:
+            engines = [Engine(B, res, res, dtype=args.dtype, seed=m, train=False, conv_math=math, tiles=args.tiles)
+                       for m in range(args.members)]
+        else:                # every member's layer in one grouped launch (jr.ensemble)
+            from jr.ensemble import EnsembleEngine
+            from jr.inception import build_inception_v3
+            from jr.init import init_params
+            g = build_inception_v3(res, res)
+            engines = EnsembleEngine([init_params(g, m) for m in range(args.members)], B, res, res,
+                                     dtype=args.dtype, conv_math=math, tiles=args.tiles)
         evaluate.predict_all(engines, d, B)          # warm-up pass (decoder threads, tiles, caches)
         t0 = time.perf_counter()
         preds, labels, _ = evaluate.predict_all(engines, d, B)
@@ -281,15 +291,16 @@ def ensemble_bench(args) -> dict:
         lib.dataset.close_iterator(it)
         t_dec = time.perf_counter() - t0
         x, y = batches[0]
-        for e in engines:
+        group = engines if args.per_member else [engines]
+        for e in group:
             e.set_batch(x, y)
             e.forward()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(len(batches)):
-            for e in engines:
+            for e in group:
                 e.forward()
-        for e in engines:
+        for e in group:
             e.synchronize()
         t_gpu = time.perf_counter() - t0
     finally:
@@ -304,8 +315,10 @@ def ensemble_bench(args) -> dict:
                 f"init per member",
         "config": {"workload": f"evaluate.predict_all: {M} resident members x {-(-n // B)} batches of {B}, each "
                                f"batch read + decoded once (native JPEG, {evaluate.NUM_WORKERS} threads) and run "
-                               f"through every member", "model": "inception_v3", "global_batch": B, "seq_len": None,
-                   "parallelism": "dp1", "members": M, "tiles": engines[0].tiles},
+                               f"through every member ({'one engine per member' if args.per_member else 'every member in one grouped launch per layer'})",
+                   "model": "inception_v3", "global_batch": B, "seq_len": None,
+                   "parallelism": "dp1", "members": M, "tiles": group[0].tiles,
+                   "grouped": not args.per_member},
         "member_images_per_s": round(n * M / t_all, 1),
         "decode_only_images_per_s": round(n / t_dec, 1),
         "gpu_forward_only_images_per_s": round(n / t_gpu, 1),

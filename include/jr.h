@@ -120,6 +120,21 @@ int jr_conv2d_fwd(const jr_conv_desc* d, int dtype, const void* x, const void* w
  * in a fixed order: deterministic.  Replaces jr_conv2d_fwd + jr_bn_stats. */
 int jr_conv2d_fwd_bn_stats(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y, float eps,
                            float* mean, float* invstd, void* ws, size_t ws_bytes, void* stream);
+/* Grouped jr_conv2d_fwd_bn_stats for the members of an ensemble (evaluate.py
+ * -lm: the same layer of `members` models over the same batch, replacing the
+ * reference's per-model sess.run of evaluate.py:166-211): ONE launch per GEMM,
+ * member i reading x + i*x_member_stride and w + i*w_member_stride and
+ * writing y + i*y_member_stride, mean / invstd + i*stats_member_stride
+ * (strides in elements of each tensor; w = the filter operand of that dtype:
+ * fp32 HWIO, or the bf16 W^T copy for JR_BF16).  dtype JR_F32, JR_BF16 or
+ * JR_F32_X8.  Each member's plan (tile, split-K) is the per-member plan, so
+ * its y, mean and invstd are bitwise those of jr_conv2d_fwd_bn_stats on its
+ * own tensors.  Workspace: jr_conv2d_workspace_size_grouped. */
+size_t jr_conv2d_workspace_size_grouped(const jr_conv_desc* d, int dtype, int members);
+int jr_conv2d_fwd_bn_stats_grouped(const jr_conv_desc* d, int dtype, int members, const void* x,
+                                   int64_t x_member_stride, const void* w, int64_t w_member_stride, void* y,
+                                   int64_t y_member_stride, float eps, float* mean, float* invstd,
+                                   int64_t stats_member_stride, void* ws, size_t ws_bytes, void* stream);
 /* dx[.., x_c_off + ci] (+)= sum dy * w ; accumulate != 0 adds into dx */
 int jr_conv2d_bwd_data(const jr_conv_desc* d, int dtype, const void* dy, const void* w, void* dx,
                        int accumulate, void* ws, size_t ws_bytes, void* stream);
@@ -183,6 +198,13 @@ int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps, float
 int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,
                      const float* mean, const float* invstd, const float* beta, void* y, int32_t y_c_off,
                      int32_t y_c_stride, void* stream);
+/* jr_bn_relu_apply for the members of an ensemble in one launch: member i
+ * reads x + i*x_member_stride, mean / invstd + i*stats_member_stride, beta +
+ * i*beta_member_stride and writes y + i*y_member_stride (elements). */
+int jr_bn_relu_apply_grouped(int dtype, int32_t members, const void* x, int32_t x_c_off, int32_t x_c_stride,
+                             int64_t x_member_stride, int64_t m, int32_t c, const float* mean, const float* invstd,
+                             int64_t stats_member_stride, const float* beta, int64_t beta_member_stride, void* y,
+                             int32_t y_c_off, int32_t y_c_stride, int64_t y_member_stride, void* stream);
 /* Backward of apply+stats: dy is the gradient w.r.t. y (a channel slice),
  * dx receives the gradient w.r.t. the raw conv output in the same channel
  * slice geometry as x, dbeta [c] receives sum of the ReLU-masked dy. */

@@ -328,12 +328,23 @@ __global__ void __launch_bounds__(256) k_bn_finalize(const double* __restrict__ 
 
 // Elementwise passes: block b covers rows [b*rpp*U, (b+1)*rpp*U), thread
 // (q, rr) rows rr, rr+rpp, ...; per-channel constants loaded once.
+// Grouped (ensemble members, blockIdx.y = member): x, y, the statistics and
+// beta move by their member strides (bytes; all 0 for an ordinary launch).
 template <typename T>
 __global__ void __launch_bounds__(256) k_bn_relu_apply(const T* __restrict__ x, int xs, int64_t m, int c,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
                                                        const float* __restrict__ beta, T* y, int y_off,
-                                                       int y_stride) {
+                                                       int y_stride, int64_t x_mb, int64_t y_mb, int64_t st_mb,
+                                                       int64_t be_mb) {
+  if (gridDim.y > 1) {
+    const int64_t mb = blockIdx.y;
+    x = reinterpret_cast<const T*>(reinterpret_cast<const char*>(x) + mb * x_mb);
+    y = reinterpret_cast<T*>(reinterpret_cast<char*>(y) + mb * y_mb);
+    mean = reinterpret_cast<const float*>(reinterpret_cast<const char*>(mean) + mb * st_mb);
+    invstd = reinterpret_cast<const float*>(reinterpret_cast<const char*>(invstd) + mb * st_mb);
+    beta = reinterpret_cast<const float*>(reinterpret_cast<const char*>(beta) + mb * be_mb);
+  }
   constexpr int VW = Vec<T>::N;
   const int tpr = c / VW;
   const int rpp = 256 / tpr;
@@ -482,6 +493,19 @@ JR_API int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps
   return check_launch("bn_stats finalize");
 }
 
+static int bn_apply_launch(int dtype, int members, const void* x, int32_t x_c_stride, int64_t x_mb, int64_t m,
+                           int32_t c, const float* mean, const float* invstd, int64_t st_mb, const float* beta,
+                           int64_t be_mb, void* y, int32_t y_c_off, int32_t y_c_stride, int64_t y_mb, hipStream_t s) {
+  const dim3 grid(apply_grid(m, c, vec_width(dtype)), members);
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_bn_relu_apply<float>, grid, dim3(256), 0, s, (const float*)x, x_c_stride, m, c, mean,
+                       invstd, beta, (float*)y, y_c_off, y_c_stride, x_mb, y_mb, st_mb, be_mb);
+  else
+    hipLaunchKernelGGL(k_bn_relu_apply<uint16_t>, grid, dim3(256), 0, s, (const uint16_t*)x, x_c_stride, m, c,
+                       mean, invstd, beta, (uint16_t*)y, y_c_off, y_c_stride, x_mb, y_mb, st_mb, be_mb);
+  return check_launch("bn_relu_apply");
+}
+
 JR_API int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,
                             const float* mean, const float* invstd, const float* beta, void* y, int32_t y_c_off,
                             int32_t y_c_stride, void* stream) {
@@ -492,15 +516,30 @@ JR_API int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x
   const size_t esz = dtype == JR_BF16 ? 2 : 4;
   x = static_cast<const char*>(x) + (size_t)x_c_off * esz;
   if (!check_slice(dtype, y_c_off, y_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_apply: bad output slice");
-  hipStream_t s = as_stream(stream);
-  const int grid = apply_grid(m, c, vec_width(dtype));
-  if (dtype == JR_F32)
-    hipLaunchKernelGGL(k_bn_relu_apply<float>, dim3(grid), dim3(256), 0, s, (const float*)x, x_c_stride, m, c, mean,
-                       invstd, beta, (float*)y, y_c_off, y_c_stride);
-  else
-    hipLaunchKernelGGL(k_bn_relu_apply<uint16_t>, dim3(grid), dim3(256), 0, s, (const uint16_t*)x, x_c_stride, m, c,
-                       mean, invstd, beta, (uint16_t*)y, y_c_off, y_c_stride);
-  return check_launch("bn_relu_apply");
+  return bn_apply_launch(dtype, 1, x, x_c_stride, 0, m, c, mean, invstd, 0, beta, 0, y, y_c_off, y_c_stride, 0,
+                         as_stream(stream));
+}
+
+JR_API int jr_bn_relu_apply_grouped(int dtype, int32_t members, const void* x, int32_t x_c_off, int32_t x_c_stride,
+                                    int64_t x_member_stride, int64_t m, int32_t c, const float* mean,
+                                    const float* invstd, int64_t stats_member_stride, const float* beta,
+                                    int64_t beta_member_stride, void* y, int32_t y_c_off, int32_t y_c_stride,
+                                    int64_t y_member_stride, void* stream) {
+  int rc = check_common(dtype, m, c);
+  if (rc) return rc;
+  if (members < 1 || members > 65535) return fail(JR_ERR_INVALID, "bn_relu_apply_grouped: members must be 1..65535");
+  if (!x || !mean || !invstd || !beta || !y) return fail(JR_ERR_INVALID, "bn_relu_apply_grouped: null pointer");
+  if (x_member_stride < 0 || y_member_stride < 0 || stats_member_stride < 0 || beta_member_stride < 0)
+    return fail(JR_ERR_INVALID, "bn_relu_apply_grouped: negative member stride");
+  if (!check_slice(dtype, x_c_off, x_c_stride, c) || !check_slice(dtype, y_c_off, y_c_stride, c))
+    return fail(JR_ERR_INVALID, "bn_relu_apply_grouped: bad input / output slice");
+  const size_t esz = dtype == JR_BF16 ? 2 : 4;
+  if (((x_member_stride * esz) | (y_member_stride * esz)) & 15)
+    return fail(JR_ERR_INVALID, "bn_relu_apply_grouped: member strides must be 16-byte multiples");
+  x = static_cast<const char*>(x) + (size_t)x_c_off * esz;
+  return bn_apply_launch(dtype, members, x, x_c_stride, x_member_stride * esz, m, c, mean, invstd,
+                         stats_member_stride * 4, beta, beta_member_stride * 4, y, y_c_off, y_c_stride,
+                         y_member_stride * esz, as_stream(stream));
 }
 
 // The apply pass of the backward (k1, k2 from a finalize).

@@ -148,6 +148,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int SMEM = NBUF * (ASZ + BSZ) > 4 * stage_floats<WN>() ? NBUF * (ASZ + BSZ) : 4 * stage_floats<WN>();
   __shared__ __attribute__((aligned(1024))) float smem[SMEM];
   JR_ST(Stamps stamp; stamp.start();)
+  member_offsets(g);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -936,10 +937,22 @@ JR_API int jr_debug_set_stamps(void* p) {
 // One GEMM (plus its split-K reduce) on the stream.
 // defer (WGRAD): write the split-K slabs into ws and stop (jr_wgrad_reduce
 // sums them later, batched with other layers').
+// Workspace of one member of a grouped GEMM: split-K slabs, then the fused
+// BN statistics partials (their two-stage combine space included).
+static size_t member_ws(int dtype, const Plan& p, bool stats) {
+  return align256(stats ? align256(plan_ws(p)) + stats_ws(dtype, p) : plan_ws(p));
+}
+
 template <int OP>
 static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, size_t ws_bytes, hipStream_t s,
-                    const StatsReq* st = nullptr, bool defer = false) {
+                    const StatsReq* st = nullptr, bool defer = false, int members = 1, long long st_mb = 0) {
   if (p.M <= 0 || p.N <= 0) return JR_OK;
+  // grouped (members > 1): every member's GEMM in one launch (blockIdx.y),
+  // each with its own workspace region of member_ws bytes; a.a_mb / b_mb /
+  // o_mb (operand and output strides) are the caller's
+  const size_t wsm = members > 1 ? member_ws(dtype, p, st != nullptr) : 0;
+  if (members > 1 && (!ws || ws_bytes < wsm * members) && (p.splits > 1 || st))
+    return fail(JR_ERR_WORKSPACE, "conv grouped: workspace too small (jr_conv2d_workspace_size_grouped)");
   int sP = 0, sR = 0;
   if (st) {
     stats_geom(dtype, p, &sP, &sR);
@@ -947,6 +960,7 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     if (!ws || ws_bytes < off + stats_ws(dtype, p)) return fail(JR_ERR_WORKSPACE, "conv: workspace too small for BN statistics");
     a.stats = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
     a.stats_p = sP;
+    a.s_mb = (long long)wsm;
   }
   a.M = p.M; a.N = p.N; a.K = p.K;
   JR_ST(a.dbg = g_dbg_stamps;)
@@ -957,10 +971,12 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
   if (p.splits > 1) {
     if (!ws || ws_bytes < plan_ws(p)) return fail(JR_ERR_WORKSPACE, "conv: workspace too small for split-K");
     a.C = static_cast<float*>(ws);
+    a.c_mb = (long long)wsm;
   } else {
     a.C = static_cast<float*>(out);
+    a.c_mb = a.o_mb;
   }
-  dim3 grid(p.mt * p.nt, 1, p.splits);
+  dim3 grid(p.mt * p.nt, members, p.splits);
   if (is_halo(dtype, p.tile)) {
     const HaloCfg& h = kHaloBf16[p.tile - kNumCfgsBf16];
     a.halo_wp = a.w + a.kw - 1;
@@ -995,31 +1011,36 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
   if (rc) return rc;
   if (st) {
     if (p.splits > 1) {
+      const dim3 rg(sP, (int)ceil_div(p.N, 1024), members);
       if (dtype == JR_BF16)
-        hipLaunchKernelGGL((k_splitk_reduce_stats<uint16_t>), dim3(sP, (int)ceil_div(p.N, 1024)), dim3(256), 0, s, (const float*)ws, p.splits, a,
+        hipLaunchKernelGGL((k_splitk_reduce_stats<uint16_t>), rg, dim3(256), 0, s, (const float*)ws, p.splits, a,
                            static_cast<uint16_t*>(out), sR);
       else
-        hipLaunchKernelGGL((k_splitk_reduce_stats<float>), dim3(sP, (int)ceil_div(p.N, 1024)), dim3(256), 0, s, (const float*)ws, p.splits, a,
+        hipLaunchKernelGGL((k_splitk_reduce_stats<float>), rg, dim3(256), 0, s, (const float*)ws, p.splits, a,
                            static_cast<float*>(out), sR);
       rc = check_launch("conv split-k reduce + stats");
       if (rc) return rc;
     }
+    const long long pm = (long long)wsm;   // partials' member stride
     if (sP <= kStatsChunk) {
-      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N), dim3(256), 0, s, (const float*)a.stats, (const float*)nullptr,
-                         sP, sR, p.M, p.N, sP, st->eps, st->mean, st->invstd, (float*)nullptr);
+      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N, 1, members), dim3(256), 0, s, (const float*)a.stats,
+                         (const float*)nullptr, sP, sR, p.M, p.N, sP, st->eps, st->mean, st->invstd, (float*)nullptr,
+                         pm, st_mb);
     } else {   // two stages: per-chunk (mean, M2, n), then the final combine
       const int S = (int)ceil_div(sP, kStatsChunk);
       float* s2 = a.stats + 2 * (size_t)p.N * sP;
-      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N, S), dim3(256), 0, s, (const float*)a.stats, (const float*)nullptr,
-                         sP, sR, p.M, p.N, kStatsChunk, st->eps, (float*)nullptr, (float*)nullptr, s2);
+      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N, S, members), dim3(256), 0, s, (const float*)a.stats,
+                         (const float*)nullptr, sP, sR, p.M, p.N, kStatsChunk, st->eps, (float*)nullptr,
+                         (float*)nullptr, s2, pm, st_mb);
       rc = check_launch("conv stats combine");
       if (rc) return rc;
-      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N), dim3(256), 0, s, (const float*)s2,
+      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N, 1, members), dim3(256), 0, s, (const float*)s2,
                          (const float*)(s2 + 2 * (size_t)p.N * S), S, 0, p.M, p.N, S, st->eps, st->mean, st->invstd,
-                         (float*)nullptr);
+                         (float*)nullptr, pm, st_mb);
     }
     return check_launch("conv stats finalize");
   }
+  if (members > 1) return fail(JR_ERR_UNSUPPORTED, "conv grouped: forward with BN statistics only");
   if (p.splits <= 1 || defer) return rc;
   const long long total = (long long)p.M * p.N / 4;   // float4 columns
   const int G = reduce_lanes(p);                       // z-lanes per column
@@ -1220,7 +1241,16 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
 // (mean, invstd), else it writes one (mean, M2, count) partial per chunk.
 __global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict__ part, const float* __restrict__ cnt,
                                                         int P, int R, int M, int N, int chunk, float eps,
-                                                        float* mean, float* invstd, float* out) {
+                                                        float* mean, float* invstd, float* out, long long p_mb,
+                                                        long long st_mb) {
+  if (gridDim.z > 1) {   // grouped: member blockIdx.z (partials / counts / out by p_mb, results by st_mb)
+    const long long mz = blockIdx.z;
+    part = reinterpret_cast<const float*>(reinterpret_cast<const char*>(part) + mz * p_mb);
+    if (cnt) cnt = reinterpret_cast<const float*>(reinterpret_cast<const char*>(cnt) + mz * p_mb);
+    if (out) out = reinterpret_cast<float*>(reinterpret_cast<char*>(out) + mz * p_mb);
+    if (mean) mean = reinterpret_cast<float*>(reinterpret_cast<char*>(mean) + mz * st_mb);
+    if (invstd) invstd = reinterpret_cast<float*>(reinterpret_cast<char*>(invstd) + mz * st_mb);
+  }
   __shared__ double red[3][256];
   const int n = blockIdx.x, t = threadIdx.x;
   const float* pm = part + (long long)n * P;
@@ -1381,6 +1411,45 @@ JR_API int jr_conv2d_fwd_bn_stats(const jr_conv_desc* d, int dtype, const void* 
   if (!mean || !invstd) return fail(JR_ERR_INVALID, "conv fwd+stats: null statistics pointer");
   const StatsReq st{eps, mean, invstd};
   return run_conv(d, OP_FWD, dtype, x, w, y, 0, ws, ws_bytes, stream, -1, -1, &st);
+}
+
+// Grouped forward (ensemble members): the same conv geometry for `members`
+// models in ONE launch per GEMM (blockIdx.y = member), each member with its
+// own input, filter, output and BN statistics at the given element strides;
+// the plan (tile, split-K) is the per-member plan, so every member's result
+// is bitwise that of jr_conv2d_fwd_bn_stats on its own tensors.
+JR_API size_t jr_conv2d_workspace_size_grouped(const jr_conv_desc* d, int dtype, int members) {
+  if (!d || members < 1 || validate(d, OP_FWD, dtype) != JR_OK) return 0;
+  return (size_t)members * align256(ws_bytes_for(d, OP_FWD, dtype));
+}
+
+JR_API int jr_conv2d_fwd_bn_stats_grouped(const jr_conv_desc* d, int dtype, int members, const void* x,
+                                          int64_t x_member_stride, const void* w, int64_t w_member_stride, void* y,
+                                          int64_t y_member_stride, float eps, float* mean, float* invstd,
+                                          int64_t stats_member_stride, void* ws, size_t ws_bytes, void* stream) {
+  int rc = validate(d, OP_FWD, dtype);
+  if (rc) return rc;
+  if (dtype != JR_F32 && dtype != JR_BF16 && dtype != JR_F32_X8)
+    return fail(JR_ERR_UNSUPPORTED, "conv grouped: dtype must be JR_F32, JR_BF16 or JR_F32_X8");
+  if (members < 1 || members > 65535) return fail(JR_ERR_INVALID, "conv grouped: members must be 1..65535");
+  if (!x || !w || !y || !mean || !invstd) return fail(JR_ERR_INVALID, "conv grouped: null pointer");
+  const long long esz = dtype == JR_BF16 ? 2 : 4;
+  if ((((uintptr_t)x | (uintptr_t)w | (uintptr_t)y) & 15) ||
+      ((x_member_stride * esz) | (w_member_stride * esz) | (y_member_stride * esz)) & 15 ||
+      x_member_stride < 0 || w_member_stride < 0 || y_member_stride < 0 || stats_member_stride < 0)
+    return fail(JR_ERR_INVALID, "conv grouped: tensors and member strides must be 16-byte aligned, strides >= 0");
+  ConvArgs a{};
+  fill_common(a, d, dtype);
+  a.A = static_cast<const float*>(x);
+  a.B = static_cast<const float*>(w);
+  a.accumulate = 0;
+  a.a_mb = x_member_stride * esz;
+  a.b_mb = w_member_stride * esz;
+  a.o_mb = y_member_stride * esz;
+  a.c_off = d->y_c_off; a.c_stride = d->y_c_stride;
+  const StatsReq st{eps, mean, invstd};
+  return run_gemm<OP_FWD>(dtype, a, plan_for(d, OP_FWD, dtype, nullptr), y, ws, ws_bytes, as_stream(stream), &st,
+                          false, members, stats_member_stride * 4);
 }
 
 JR_API size_t jr_conv2d_workspace_size(const jr_conv_desc* d, int op, int dtype) {

@@ -67,6 +67,7 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
   __shared__ __attribute__((aligned(1024))) uint16_t smem[SMEM];
 
   JR_ST(Stamps stamp; stamp.start();)
+  member_offsets(g);
   const uint16_t* __restrict__ gA = reinterpret_cast<const uint16_t*>(g.A);
   const uint16_t* __restrict__ gB = reinterpret_cast<const uint16_t*>(g.B);
   const int tid = threadIdx.x;

@@ -46,6 +46,7 @@ __global__ void __launch_bounds__(256) k_conv_halo(ConvArgs g) {
   constexpr int per_tile = A_INSTR / 4 + B_INSTR / 4;       // DMA instructions per wave and chunk (min)
   constexpr int KSTEPS = 2 * TAPS;                          // 16-channel MFMA steps per chunk
 
+  member_offsets(g);
   const uint16_t* __restrict__ gA = reinterpret_cast<const uint16_t*>(g.A);
   const uint16_t* __restrict__ gB = reinterpret_cast<const uint16_t*>(g.B);
   const int tid = threadIdx.x;

@@ -41,7 +41,24 @@ struct ConvArgs {
   // diagnostic builds only (-DJR_STAMPS, `make stamps`): per-block s_memtime /
   // s_memrealtime stamps, 8 per block (jr_debug_set_stamps); nullptr otherwise
   unsigned long long* dbg;
+  // grouped launches (ensemble members, jr_conv2d_fwd_bn_stats_grouped): the
+  // member is blockIdx.y of the GEMM; byte strides between consecutive
+  // members of A, B, C (the output, or the member's split-K slab region),
+  // the statistics partials and the final output (split-K reduce)
+  long long a_mb, b_mb, c_mb, s_mb, o_mb;
 };
+
+// Moves a grouped GEMM's operand / output pointers to member blockIdx.y
+// (a no-op for ordinary launches, gridDim.y == 1).
+__device__ __forceinline__ void member_offsets(ConvArgs& g) {
+  if (gridDim.y > 1) {
+    const long long m = blockIdx.y;
+    g.A = reinterpret_cast<const float*>(reinterpret_cast<const char*>(g.A) + m * g.a_mb);
+    g.B = reinterpret_cast<const float*>(reinterpret_cast<const char*>(g.B) + m * g.b_mb);
+    g.C = reinterpret_cast<float*>(reinterpret_cast<char*>(g.C) + m * g.c_mb);
+    if (g.stats) g.stats = reinterpret_cast<float*>(reinterpret_cast<char*>(g.stats) + m * g.s_mb);
+  }
+}
 
 #ifdef JR_STAMPS
 // [0] realtime at start, [1] realtime at end (100 MHz), [2] cycles of the
@@ -357,6 +374,12 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
 template <typename TO>
 __global__ void __launch_bounds__(256) k_splitk_reduce_stats(const float* __restrict__ slab, int splits, ConvArgs g,
                                                              TO* out, int R) {
+  if (gridDim.z > 1) {   // grouped: member blockIdx.z
+    const long long mz = blockIdx.z;
+    slab = reinterpret_cast<const float*>(reinterpret_cast<const char*>(slab) + mz * g.c_mb);
+    out = reinterpret_cast<TO*>(reinterpret_cast<char*>(out) + mz * g.o_mb);
+    g.stats = reinterpret_cast<float*>(reinterpret_cast<char*>(g.stats) + mz * g.s_mb);
+  }
   __shared__ float s_n[256];
   __shared__ float4 s_mu[256], s_m2[256];
   const int cb = blockIdx.y * 1024;
@@ -452,7 +475,8 @@ __global__ void __launch_bounds__(256) k_splitk_reduce_stats(const float* __rest
 // large).
 __global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict__ part, const float* __restrict__ cnt,
                                                         int P, int R, int M, int N, int chunk, float eps,
-                                                        float* mean, float* invstd, float* out);
+                                                        float* mean, float* invstd, float* out, long long p_mb,
+                                                        long long st_mb);
 
 struct TileCfg {
   int bm, bn, wgm, bk, nbuf;

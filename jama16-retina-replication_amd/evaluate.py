@@ -64,6 +64,9 @@ def build_parser():
     p.add_argument("--conv_math", default="x8", choices=["x8", "x8p", "f32"],
                    help="fp32 convolution arithmetic: x8 = exact 3-way bf16 split on the matrix cores (fp32-accurate, "
                         "default), x8p = the same on pre-split operand planes, f32 = fp32 MFMA")
+    p.add_argument("--per_member", action="store_true",
+                   help="one engine per ensemble member (default: every member's layers in one grouped launch, "
+                        "jr.ensemble; predictions are bitwise the same)")
     return p
 
 
@@ -81,13 +84,19 @@ def expand_model_paths(load_model_path: str):
     return [load_model_path]
 
 
-def make_engines(paths, meta, batch_size, device=0, conv_math="x8", dtype="f32"):
-    """One inference engine per ensemble member, parameters loaded; conv
-    tiles from the committed MI355X table of the eval workload (Engine
-    tiles="pinned"; the heuristic where none matches): every member and every
-    run sums in the same order."""
+def make_engines(paths, meta, batch_size, device=0, conv_math="x8", dtype="f32", grouped=False):
+    """The ensemble's inference engines, parameters loaded; conv tiles from
+    the committed MI355X table of the eval workload (tiles="pinned"; the
+    heuristic where none matches): every member and every run sums in the
+    same order.  grouped: ONE jr.ensemble.EnsembleEngine holding every member
+    (one launch per layer for all members); else one jr.Engine per member."""
     from jr import checkpoint
     from jr.engine import Engine
+    if grouped and conv_math != "x8p":
+        from jr.ensemble import EnsembleEngine
+        params = [checkpoint.load(path, None)[0] for path in paths]
+        return EnsembleEngine(params, batch_size, meta["height"], meta["width"], meta.get("units", 1), device=device,
+                              dtype=dtype, conv_math=conv_math if dtype == "f32" else "bf16")
     engines = []
     for path in paths:
         eng = Engine(batch_size, meta["height"], meta["width"], meta.get("units", 1), device=device,
@@ -103,12 +112,14 @@ def predict_all(engines, data_dir, batch_size, rank=0, world=1):
     batch indices).  Each batch is decoded once (this rank's batches only)
     and run through every member."""
     import torch
+    grouped = hasattr(engines, "members")      # jr.ensemble.EnsembleEngine
+    g = engines.g if grouped else engines[0].g
     dataset = lib.dataset.initialize_dataset(
         data_dir, batch_size, num_workers=NUM_WORKERS, prefetch_buffer_size=2 * batch_size,
         image_data_format="channels_last", num_channels=NUM_CHANNELS,
-        image_dim=[engines[0].g.height, engines[0].g.width], decode_dtype="uint8",
+        image_dim=[g.height, g.width], decode_dtype="uint8",
         shard=(rank, world))
-    preds = [[] for _ in engines]
+    preds = [[] for _ in range(engines.members if grouped else len(engines))]
     got_y, ids = [], []
     it = iter(dataset)
     try:
@@ -118,6 +129,12 @@ def predict_all(engines, data_dir, batch_size, rank=0, world=1):
             # every member's forward is enqueued before the first result is
             # read back (one host sync per batch, not per member), while the
             # decoder threads already work on the next batches
+            if grouped:       # every member's layer in one launch
+                n = engines.set_batch(x, y)
+                engines.forward(n)
+                for m, p in enumerate(engines.predictions(n)):
+                    preds[m].append(p)
+                continue
             # (the uint8 batch crosses PCIe once for all members)
             xd = torch.as_tensor(x).to(engines[0].device)
             torch.cuda.current_stream(engines[0].device).synchronize()
@@ -209,7 +226,7 @@ Using operating treshold: {},
     thresholds = lib.metrics.generate_thresholds(NUM_THRESHOLDS, KEPSILON) + [operating_threshold]
     meta = checkpoint.read_meta(load_model_paths[0])
     engines = make_engines(load_model_paths, meta, batch_size, device=local, conv_math=args.conv_math,
-                           dtype=args.dtype)
+                           dtype=args.dtype, grouped=not args.per_member)
     preds, labels, order = predict_all(engines, data_dir, batch_size, rank, world)
 
     if dist:   # gather every rank's batches to rank 0, restore dataset order

@@ -71,6 +71,10 @@ _SIGS = {
                               c_size_t, c_void_p]),
     "jr_conv2d_fwd_bn_stats": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_float,
                                        c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "jr_conv2d_workspace_size_grouped": (c_size_t, [POINTER(ConvDesc), c_int, c_int]),
+    "jr_conv2d_fwd_bn_stats_grouped": (c_int, [POINTER(ConvDesc), c_int, c_int, c_void_p, c_int64, c_void_p, c_int64,
+                                               c_void_p, c_int64, c_float, c_void_p, c_void_p, c_int64, c_void_p,
+                                               c_size_t, c_void_p]),
     "jr_conv2d_bwd_data": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_int,
                                    c_void_p, c_size_t, c_void_p]),
     "jr_conv2d_bwd_filter": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p,
@@ -108,6 +112,9 @@ _SIGS = {
                             c_void_p, c_size_t, c_void_p]),
     "jr_bn_relu_apply": (c_int, [c_int, c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "jr_bn_relu_apply_grouped": (c_int, [c_int, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int64, c_int32,
+                                         c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int32, c_int32,
+                                         c_int64, c_void_p]),
     "jr_bn_relu_bwd": (c_int, [c_int, c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_int64, c_int32,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_size_t, c_void_p]),

@@ -1,0 +1,292 @@
+"""Grouped ensemble inference: every member of an evaluate.py -lm ensemble in
+ONE launch per layer.
+
+The reference restores and runs each ensemble member in turn
+(evaluate.py:166-211), and jr.Engine runs one member per engine.  At the
+eval batch of 32 (evaluate.py:25) most GEMMs of one member are too small to
+fill the 256 CUs (the 8x8 layers are M = 2,048 GEMMs), so members' forwards
+were underfilled launches one after another.  EnsembleEngine keeps M members
+resident as ONE replica with a member dimension: every tensor is member-major
+([member][batch ...], fixed member strides), and each layer is
+
+  * one grouped conv + BN-statistics launch (jr_conv2d_fwd_bn_stats_grouped:
+    member = blockIdx.y, each with its own weights and statistics);
+  * one grouped BN+ReLU apply per conv2d_bn layer (jr_bn_relu_apply_grouped);
+  * pools and the global average pool over M x B images (the member-major
+    activation buffers are simply a batch of M x B images);
+  * the dense / sigmoid head per member (tiny).
+
+Every member sees exactly its own batch-statistics BN (App. C Q1) and the
+per-member tile plan, so its predictions are BITWISE those of a jr.Engine of
+that member (tests/test_gpu_ensemble.py).  Inference only (train=False).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _ffi
+from .engine import DTYPES, pinned_tile_table
+from .inception import BN_EPS, build_inception_v3
+from .plan import build_plan
+
+
+class EnsembleEngine:
+    """M inference replicas (ensemble members) of one geometry on one GPU."""
+
+    def __init__(self, params: List[np.ndarray], batch: int, height: int = 299, width: int = 299, units: int = 1,
+                 device: int | torch.device = 0, dtype: str = "f32", conv_math: Optional[str] = None,
+                 tiles: str = "pinned", head: str = "sigmoid"):
+        if dtype not in DTYPES:
+            raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
+        if conv_math is None:
+            conv_math = "x8" if dtype == "f32" else "bf16"
+        if (dtype == "f32" and conv_math not in ("x8", "f32")) or (dtype == "bf16" and conv_math != "bf16"):
+            raise ValueError("grouped conv math: 'x8' or 'f32' for dtype f32, 'bf16' for dtype bf16")
+        if not torch.cuda.is_available():
+            raise RuntimeError("jr.EnsembleEngine needs a ROCm GPU (libjr has no CPU path)")
+        if not params:
+            raise ValueError("at least one member")
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        _ffi.init(self.device.index or 0)
+        self.lib = _ffi.load()
+        self.g = build_inception_v3(height, width, units)
+        self.units = self.g.units
+        self.plan = build_plan(self.g, True)
+        self.cunits = self.plan.units
+        self.nparam = self.plan.nparam
+        self.members = len(params)
+        self.batch = int(batch)
+        self.dtype, self.dt = dtype, DTYPES[dtype]
+        self.conv_math = conv_math
+        self.cdt = _ffi.JR_F32_X8 if conv_math == "x8" else self.dt
+        self.esz = 2 if self.dt == _ffi.JR_BF16 else 4
+        self.head_mode = _ffi.JR_HEAD_SIGMOID if head == "sigmoid" else _ffi.JR_HEAD_SOFTMAX
+        self.stream = torch.cuda.Stream(device=self.device)
+        self._s = ctypes.c_void_p(self.stream.cuda_stream)
+        self._alloc()
+        self.load_params(params)
+        self.tiles = "heuristic"
+        if tiles == "pinned":
+            t = pinned_tile_table(conv_math, self.batch, height, width, False)
+            if t is not None and all(u.name in t["configs"] for u in self.cunits):
+                self._apply_configs(t["configs"])
+                self.tiles = "pinned"
+        elif tiles != "heuristic":
+            raise ValueError("tiles: 'pinned' or 'heuristic'")
+        self._gen = self.lib.jr_conv2d_config_generation()
+        self._calls = {}
+
+    # ------------------------------------------------------------------ memory
+    def _t(self, n: int, dtype=torch.float32) -> torch.Tensor:
+        return torch.zeros(int(n), dtype=dtype, device=self.device)
+
+    def _alloc(self) -> None:
+        g, B, M = self.g, self.batch, self.members
+        at = torch.bfloat16 if self.dt == _ffi.JR_BF16 else torch.float32
+        q = 8 if self.dt == _ffi.JR_BF16 else 4
+        self.in_stride = (g.bufs[g.input_buf].c + q - 1) // q * q
+        # member stride of every activation buffer: one member's B images
+        self.act_ms = [B * b.h * b.w * (self.in_stride if b.id == g.input_buf else b.c) for b in g.bufs]
+        self.acts = [self._t(M * n, at) for n in self.act_ms]
+        self.raw_ms = {u.first.idx: B * u.ho * u.wo * u.cout for u in self.cunits}
+        self.raw_unit = {k: self._t(M * n, at) for k, n in self.raw_ms.items()}
+        self.stats_ms = 2 * sum(u.cout for u in self.cunits)
+        self.stats = self._t(M * self.stats_ms)
+        self.stat_off, off = {}, 0
+        for u in self.cunits:
+            self.stat_off[u.first.idx] = off
+            off += 2 * u.cout
+        feat_c = g.bufs[g.output_buf].c
+        self.feat = self._t(M * B * feat_c)
+        self.logits = self._t(M * B * self.units)
+        self.probs = self._t(M * B * self.units)
+        self.labels = self._t(B * self.units)
+        self.loss = self._t(4 * M)
+        self.params = self._t(M * self.nparam)
+        if self.dt == _ffi.JR_BF16:
+            # the bf16 W^T operand copies of every member (weights never change
+            # in inference: prepared once, at load_params)
+            layers, tiles, to = [], 0, 0
+            self.wb_t_off = {}
+            per = []
+            for u in self.cunits:
+                c8 = (u.cin + 7) // 8 * 8
+                per.append((u, to, tiles))
+                self.wb_t_off[u.first.idx] = to
+                tiles += self.lib.jr_conv_weights_bf16_tiles(u.kh, u.kw, u.cin, u.cout)
+                to += u.cout * u.kh * u.kw * c8
+            self.wt_ms = (to + 7) // 8 * 8
+            for m in range(M):
+                for u, o, t0 in per:
+                    layers.append(_ffi.WPrep(m * self.nparam + u.koff, 0, m * self.wt_ms + o, u.kh, u.kw, u.cin,
+                                             u.cout, m * tiles + t0, 0))
+            arr = (_ffi.WPrep * len(layers))(*layers)
+            self.wprep_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
+            self.wprep_layers, self.wprep_tiles = len(layers), M * tiles
+            self.w_t = self._t(M * self.wt_ms, torch.bfloat16)
+        ws = 0
+        for u in self.cunits:
+            d = self._conv_desc(u, B)
+            ws = max(ws, self.lib.jr_conv2d_workspace_size_grouped(ctypes.byref(d), self.cdt, M))
+        self.ws_bytes = int(ws)
+        self.ws = self._t((self.ws_bytes + 15) // 4 + 4)
+
+    def load_params(self, params: List[np.ndarray]) -> None:
+        """Keras-layout flat parameters of every member (jr.checkpoint.load)."""
+        if len(params) != self.members:
+            raise ValueError(f"expected {self.members} members' parameters, got {len(params)}")
+        with torch.cuda.stream(self.stream):     # ordered before the weight prep below
+            for m, flat in enumerate(params):
+                self.params[m * self.nparam:(m + 1) * self.nparam].copy_(
+                    torch.from_numpy(self.plan.to_internal(self.g, flat)).to(self.device))
+        if self.dt == _ffi.JR_BF16:
+            with torch.cuda.stream(self.stream):
+                _ffi.check("wprep", self.lib.jr_conv_weights_bf16_multi(
+                    self.wprep_table.data_ptr(), self.wprep_layers, self.wprep_tiles, self.params.data_ptr(), None,
+                    self.w_t.data_ptr(), self._s))
+        self.stream.synchronize()
+
+    # ------------------------------------------------------------ descriptors
+    def _conv_desc(self, u, B: int) -> _ffi.ConvDesc:
+        xs = self.in_stride if u.x == self.g.input_buf else u.cin
+        return _ffi.ConvDesc(B, u.h, u.w, u.cin, u.cout, u.kh, u.kw, u.stride, u.stride,
+                             u.pad_h, u.pad_w, u.ho, u.wo, 0, xs, 0, u.cout)
+
+    def _apply_configs(self, cfgs: dict) -> None:
+        """The per-member forward tile of every launch (the eval table's)."""
+        self._cfgs = cfgs
+        for u in self.cunits:
+            d = self._conv_desc(u, self.batch)
+            _ffi.check("set_config", self.lib.jr_conv2d_set_config(ctypes.byref(d), _ffi.JR_CONV_FWD, self.cdt, 0,
+                                                                   cfgs[u.name][0]))
+
+    def _p(self, m: int, name: str) -> int:
+        return self.params.data_ptr() + 4 * (m * self.nparam + self.plan.poff[name])
+
+    # ------------------------------------------------------------- call list
+    def _build_calls(self, B: int):
+        if getattr(self, "_cfgs", None) is not None and self.lib.jr_conv2d_config_generation() != self._gen:
+            self._apply_configs(self._cfgs)        # another caller moved this geometry's tiles
+            self._calls.clear()
+            self._gen = self.lib.jr_conv2d_config_generation()
+        if B in self._calls:
+            return self._calls[B]
+        if B > self.batch or B <= 0:
+            raise ValueError(f"batch {B} outside 1..{self.batch}")
+        L, g, M, s = self.lib, self.g, self.members, self._s
+        calls, keep = [], []
+        A = lambda bid: self.acts[bid].data_ptr()  # noqa: E731
+        ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
+        for n in g.nodes:
+            if n.kind == "conv":
+                u = self.plan.unit_of[n.idx]
+                if u.first is not n:
+                    continue
+                d = self._conv_desc(u, B)
+                keep.append(d)
+                uid = u.first.idx
+                so = self.stat_off[uid]
+                if self.dt == _ffi.JR_BF16:
+                    w, w_ms = self.w_t.data_ptr() + 2 * self.wb_t_off[uid], self.wt_ms
+                else:
+                    w, w_ms = self.params.data_ptr() + 4 * u.koff, self.nparam
+                raw = self.raw_unit[uid].data_ptr()
+                mean = self.stats.data_ptr() + 4 * so
+                inv = mean + 4 * u.cout
+                calls.append((L.jr_conv2d_fwd_bn_stats_grouped,
+                              (ctypes.byref(d), self.cdt, M, A(u.x), self.act_ms[u.x], w, w_ms, raw,
+                               self.raw_ms[uid], BN_EPS, mean, inv, self.stats_ms, ws, wsb, s), "conv_fwd"))
+                rows = B * u.ho * u.wo
+                for mem, co in zip(u.members, u.col_off):
+                    yb = g.bufs[mem.y.buf]
+                    calls.append((L.jr_bn_relu_apply_grouped,
+                                  (self.dt, M, raw, co, u.cout, self.raw_ms[uid], rows, mem.cout, mean + 4 * co,
+                                   inv + 4 * co, self.stats_ms, self._p(0, f"batch_normalization_{mem.idx + 1}/beta"),
+                                   self.nparam, A(mem.y.buf), mem.y.c_off, yb.c, self.act_ms[mem.y.buf], s),
+                                  "bn_relu"))
+            else:
+                # pools: the member-major buffers of a full batch are one
+                # batch of M * B images (one launch); a partial last batch
+                # (B < planned: members sit `batch` images apart) runs per member
+                yb = g.bufs[n.y.buf]
+                full = B == self.batch
+                for m in range(1 if full else M):
+                    d = _ffi.PoolDesc(M * B if full else B, n.h, n.w, n.c, n.ho, n.wo, 0, n.c, n.y.c_off, yb.c)
+                    keep.append(d)
+                    xi = A(n.x) + self.esz * m * self.act_ms[n.x]
+                    yo = A(n.y.buf) + self.esz * m * self.act_ms[n.y.buf]
+                    if n.kind == "maxpool":
+                        calls.append((L.jr_maxpool3x3s2_fwd, (ctypes.byref(d), self.dt, xi, yo, None, s),
+                                      "maxpool_fwd"))
+                    else:
+                        calls.append((L.jr_avgpool3x3s1_fwd, (ctypes.byref(d), self.dt, xi, yo, s), "avgpool_fwd"))
+        ob = g.bufs[g.output_buf]
+        if B == self.batch:
+            calls.append((L.jr_gap_fwd, (self.dt, A(g.output_buf), M * B, ob.h * ob.w, ob.c, self.feat.data_ptr(),
+                                         s), "gap_fwd"))
+        else:
+            for m in range(M):
+                calls.append((L.jr_gap_fwd, (self.dt, A(g.output_buf) + self.esz * m * self.act_ms[g.output_buf], B,
+                                             ob.h * ob.w, ob.c, self.feat.data_ptr() + 4 * m * self.batch * ob.c, s),
+                              "gap_fwd"))
+        for m in range(M):
+            f = self.feat.data_ptr() + 4 * m * self.batch * ob.c
+            o = 4 * m * self.batch * self.units
+            calls.append((L.jr_head_fwd, (self.head_mode, f, self._p(m, "dense/kernel"), self._p(m, "dense/bias"),
+                                          self.labels.data_ptr(), B, ob.c, self.units, self.logits.data_ptr() + o,
+                                          self.probs.data_ptr() + o, self.loss.data_ptr() + 16 * m, s), "head_fwd"))
+        self._calls[B] = (calls, keep)
+        return self._calls[B]
+
+    # ------------------------------------------------------------------- runs
+    def set_batch(self, images, labels=None) -> int:
+        """One batch for every member (NHWC uint8 or float32, host or device)."""
+        B = int(images.shape[0])
+        if B > self.batch or B <= 0:
+            raise ValueError(f"batch {B} outside 1..{self.batch}")
+        ib = self.g.bufs[self.g.input_buf]
+        if tuple(images.shape[1:]) != (ib.h, ib.w, ib.c):
+            raise ValueError(f"images must be [B,{ib.h},{ib.w},{ib.c}] NHWC, got {tuple(images.shape)}")
+        with torch.cuda.stream(self.stream):
+            x = torch.as_tensor(images)
+            pixels = B * ib.h * ib.w
+            dst = self.acts[self.g.input_buf]
+            if x.dtype == torch.uint8:
+                xd = x.to(self.device, non_blocking=True).reshape(-1)
+                _ffi.check("jr_image_u8_to_nhwc", self.lib.jr_image_u8_to_nhwc(
+                    xd.data_ptr(), dst.data_ptr(), self.dt, pixels, ib.c, self.in_stride, self._s))
+                self._keep_u8 = xd
+            else:
+                v = dst[:pixels * self.in_stride].view(pixels, self.in_stride)
+                v[:, ib.c:].zero_()
+                v[:, :ib.c].copy_(x.to(torch.float32).reshape(pixels, ib.c).to(self.device, non_blocking=True))
+            # every member reads the same images: copy member 0's
+            n, k = self.act_ms[self.g.input_buf], pixels * self.in_stride
+            for m in range(1, self.members):
+                dst[m * n:m * n + k].copy_(dst[:k])
+            if labels is not None:
+                y = torch.as_tensor(labels, dtype=torch.float32).reshape(-1)
+                self.labels[:y.numel()].copy_(y, non_blocking=True)
+        return B
+
+    def forward(self, B: Optional[int] = None) -> None:
+        calls, _ = self._build_calls(B or self.batch)
+        with torch.cuda.stream(self.stream):
+            for fn, args, name in calls:
+                rc = fn(*args)
+                if rc:
+                    raise _ffi.JRError(name, rc, _ffi.last_error())
+
+    def synchronize(self) -> None:
+        self.stream.synchronize()
+
+    def predictions(self, n: Optional[int] = None) -> np.ndarray:
+        """[members, n, units] sigmoid (softmax) outputs of the last forward."""
+        n = self.batch if n is None else n
+        self.synchronize()
+        p = self.probs.cpu().numpy().reshape(self.members, self.batch, self.units)
+        return p[:, :n].copy()
