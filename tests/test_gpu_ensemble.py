@@ -67,13 +67,15 @@ def _conv_case(ffi, L, dt, case, members, cfg=None, seed=3):
     if cfg is not None:
         ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, dt, 0, cfg))
     try:
-        wsb = L.jr_conv2d_workspace_size_grouped(ctypes.byref(d), dt, members)
+        # (forced split-K factors may exceed the planner's workspace bound)
+        extra = 0 if cfg is None else 4 * (cfg >> 8) * n * ho * wo * cout + (1 << 20)
+        wsb = L.jr_conv2d_workspace_size_grouped(ctypes.byref(d), dt, members) + members * extra
         ws = zeros(wsb // 4 + 4)
         Yg, Sg = zeros(members * ym, at), zeros(members * 2 * cout)
         ffi.check("grouped", L.jr_conv2d_fwd_bn_stats_grouped(
             ctypes.byref(d), dt, members, X.data_ptr(), xm, W.data_ptr(), wm, Yg.data_ptr(), ym, 1e-3,
             Sg.data_ptr(), Sg.data_ptr() + 4 * cout, 2 * cout, ws.data_ptr(), wsb, None))
-        ws1 = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, dt)
+        ws1 = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, dt) + extra
         w1 = zeros(ws1 // 4 + 4)
         esz = 2 if dt == ffi.JR_BF16 else 4
         for m in range(members):
