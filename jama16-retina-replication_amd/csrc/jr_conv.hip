@@ -129,7 +129,82 @@ struct SplitFrag {
 // (conv1, c_in = 3 padded to 4) every lane keeps its own mixed-radix k
 // counter (generic path).  WGRAD's A operand walks pixels along k, so its
 // lanes advance (b, oh, ow) counters.
-template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0>
+//
+// Stream-K (SK, the JR_F32_X8 stream-K tile ids): the grid is a fixed
+// number of blocks and the GEMM's tiles x K-tiles iterations are cut into
+// equal contiguous ranges, one per block (g.sk_ipb each), so every CU gets
+// the same MAC count whatever the tile count -- no wave quantization and no
+// split-K slabs or reduce launch.  A block walks its range tile by tile; a
+// tile cut between blocks b < b' is finished by the block holding its FIRST
+// K-tile (b, at the END of its range): every later piece is the FIRST
+// segment of blocks b+1, b+2, ..., which publish it at the START of their
+// range as an fp32 partial (write-through sc1 stores, drained, then an
+// agent-scope flag), and b adds them in block order (deterministic: the
+// cut points are fixed by the grid, the sum order by the block order) before
+// its ordinary epilogue (store + fused BN statistics).  Waits point only to
+// higher blocks, which publish before waiting on anything, so no block waits
+// on one that cannot start; spins are bounded.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sk_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void sk_publish(const ConvArgs& g, const f32x16 (&acc)[TM][TN], int wave, int lane) {
+  constexpr int SLOT = 4 * TM * TN * 16 * 64;               // floats per block slot (BM x BN)
+  const auto rs = sk_rsrc(g.sk_part + (long long)blockIdx.x * SLOT);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const i32x4 v = {__float_as_int(acc[i][j][4 * q]), __float_as_int(acc[i][j][4 * q + 1]),
+                         __float_as_int(acc[i][j][4 * q + 2]), __float_as_int(acc[i][j][4 * q + 3])};
+        const int off = (((((wave * TM + i) * TN + j) * 4 + q) * 64) + lane) * 16;
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);    // aux 16 = sc1 (write-through)
+      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(g.sk_flags + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// acc += the partial of block b (published by sk_publish), after its flag
+template <int TM, int TN>
+__device__ __forceinline__ void sk_absorb(const ConvArgs& g, f32x16 (&acc)[TM][TN], int b, int wave, int lane) {
+  constexpr int SLOT = 4 * TM * TN * 16 * 64;
+  if (threadIdx.x == 0) {            // ONE lane polls ONE word, relaxed; bounded (~1 s), then gives up
+    for (unsigned spins = 0; spins < (1u << 22); ++spins) {
+      if (__hip_atomic_load(g.sk_flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below the poll)
+  const auto rs = sk_rsrc(g.sk_part + (long long)b * SLOT);
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  // one accumulator row i at a time (TN x 4 loads in flight): the loaded
+  // partial never holds more than TN x 16 VGPRs
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    i32x4 v[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)   // every load of the hand-off sc1 (write-through producer, drained)
+        v[j][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (((((wave * TM + i) * TN + j) * 4 + q) * 64) + lane) * 16,
+                                                        0, 16);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += __int_as_float(v[j][q][e]);
+  }
+}
+
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0, bool SK = false>
 __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int WGN = 4 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -156,11 +231,31 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   const int wm0 = (wave / WGN) * WM;
   const int wn0 = (wave % WGN) * WN;
 
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  // SK: this block's iteration range [sk_it, sk_end) over tiles x K-tiles
+  long long sk_it = 0, sk_end = 0;
+  if constexpr (SK) {
+    const long long W = (long long)((g.M + BM - 1) / BM) * g.ntn * g.ktiles;
+    sk_it = (long long)blockIdx.x * g.sk_ipb;
+    sk_end = sk_it + g.sk_ipb < W ? sk_it + g.sk_ipb : W;
+  }
+  bool sk_first = true;
+  // one iteration per (tile, K range) segment: ordinary launches run exactly one
+  for (;;) {
+  int tile, kt0, kt1;
+  if constexpr (SK) {
+    if (sk_it >= sk_end) break;
+    tile = (int)(sk_it / g.ktiles);
+    kt0 = (int)(sk_it - (long long)tile * g.ktiles);
+    kt1 = (int)(sk_end - sk_it < (long long)(g.ktiles - kt0) ? kt0 + (sk_end - sk_it) : g.ktiles);
+    sk_it += kt1 - kt0;
+    if (!sk_first) __syncthreads();      // the previous segment's stage / ring reads are done
+  } else {
+    tile = xcd_remap(blockIdx.x, gridDim.x);
+    kt0 = blockIdx.z * g.kt_per_split;
+    kt1 = min(g.ktiles, kt0 + g.kt_per_split);
+  }
   const int mt = tile / g.ntn, nt = tile - mt * g.ntn;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int kt0 = blockIdx.z * g.kt_per_split;
-  const int kt1 = min(g.ktiles, kt0 + g.kt_per_split);
   const float* zp = g_zero_page;
   const int cred = OP == OP_FWD ? g.cp : g.cout;       // channel radix of the KC k index
   // FWD/DGRAD: UT = wave-uniform tap (host guarantees cred % BK == 0).
@@ -632,8 +727,21 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   }
   JR_ST(stamp.loop();)
 
+  if constexpr (SK) {
+    const bool first = sk_first;
+    sk_first = false;
+    if (kt0 != 0) {                  // (only a block's first segment starts inside a tile)
+      if (first) sk_publish<TM, TN>(g, acc, wave, lane);
+      continue;
+    }
+    // the tile's later pieces: the first segments of blocks blockIdx.x + 1, ...
+    for (int b = blockIdx.x + 1, covered = kt1; covered < g.ktiles; ++b, covered += (int)g.sk_ipb)
+      sk_absorb<TM, TN>(g, acc, b, wave, lane);
+  }
   // ---------------------------------------------------------------- epilogue
   conv_epilogue<OP, WM, TM, TN, false>(g, acc, smem + wave * stage_floats<WN>(), m0 + wm0, n0 + wn0, lane);
+  if constexpr (!SK) break;
+  }
   JR_ST(stamp.end(g.dbg);)
 }
 
@@ -657,6 +765,10 @@ struct Plan {
   int tile;
   int M, N, K;
   int mt, nt, ktiles, splits, kt_per_split;
+  // stream-K (k_conv SK): blocks and iterations (tiles x K-tiles) per block
+  bool sk;
+  int sk_blocks;
+  long long sk_ipb;
 };
 
 // Channel padding of the reduction operand: 16 B DMA pieces hold 4 fp32 or
@@ -685,17 +797,20 @@ static int wide_base(int dtype) {
 static int cfg_count(int dtype) {
   return dtype == JR_BF16 ? wide_base(dtype) + kNumCfgsBf16W
          : dtype == JR_F32_X8P ? wide_base(dtype) + kNumCfgsX8PW
-         : std_count(dtype) + (dtype == JR_F32_X8 ? kNumCfgs : 0);
+         : std_count(dtype) + (dtype == JR_F32_X8 ? 2 * kNumCfgs : 0);
 }
 static bool is_halo(int dtype, int tile) {
   return dtype == JR_BF16 && tile >= kNumCfgsBf16 && tile < kNumCfgsBf16 + kNumHaloBf16;
 }
 static bool is_wide(int dtype, int tile) { return tile >= wide_base(dtype) && tile < cfg_count(dtype); }
-static bool is_x8_f32(int dtype, int tile) { return dtype == JR_F32_X8 && tile >= kNumCfgs; }
+static bool is_x8_f32(int dtype, int tile) { return dtype == JR_F32_X8 && tile >= kNumCfgs && tile < 2 * kNumCfgs; }
+// JR_F32_X8 ids [28, 42): the stream-K grid of x8 tile (id - 28) (k_conv SK)
+static bool is_sk(int dtype, int tile) { return dtype == JR_F32_X8 && tile >= 2 * kNumCfgs; }
 static const TileCfg& tile_cfg(int dtype, int tile) {
   if (is_halo(dtype, tile)) return kHaloBf16[tile - kNumCfgsBf16].t;
   if (is_wide(dtype, tile)) return (dtype == JR_BF16 ? kCfgsBf16W : kCfgsX8PW)[tile - wide_base(dtype)];
   if (is_x8_f32(dtype, tile)) return kCfgs[tile - kNumCfgs];
+  if (is_sk(dtype, tile)) return kCfgs[tile - 2 * kNumCfgs];
   return (dtype == JR_BF16 ? kCfgsBf16 : dtype == JR_F32_X8P ? kCfgsX8P : kCfgs)[tile];
 }
 // Halo rows a BM-row tile needs: output rows it spans (bound) + kh - 1.
@@ -727,6 +842,9 @@ static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
   *nph = k;
 }
 
+constexpr int kSkBlocks = 512;     // stream-K grid: 2 x 256 CUs
+constexpr int kSkMinIters = 4;     // K-tiles per stream-K block at least
+
 static Plan plan_with(int dtype, int cfg, int M, int N, int K) {
   Plan p{};
   p.M = M; p.N = N; p.K = K; p.cfg = cfg; p.tile = cfg_tile(cfg);
@@ -743,6 +861,16 @@ static Plan plan_with(int dtype, int cfg, int M, int N, int K) {
     splits = std::min(std::min(splits, max_by_k), 256);
   }
   if (cfg_splits(cfg) > 0) splits = std::min(cfg_splits(cfg), std::max(p.ktiles, 1));
+  if (is_sk(dtype, p.tile)) {
+    // stream-K: a fixed grid (two blocks per CU at most resident; larger
+    // tiles run it in two equal rounds), at least kSkMinIters K-tiles each
+    splits = 1;
+    const long long W = (long long)tiles * std::max(p.ktiles, 1);
+    const long long P = std::max(1LL, std::min<long long>(kSkBlocks, W / kSkMinIters));
+    p.sk = true;
+    p.sk_ipb = ceil_div(W, P);
+    p.sk_blocks = (int)ceil_div(W, p.sk_ipb);
+  }
   p.kt_per_split = (int)ceil_div(std::max(p.ktiles, 1), splits);
   p.splits = (int)ceil_div(std::max(p.ktiles, 1), p.kt_per_split);
   return p;
@@ -806,7 +934,14 @@ static int reduce_lanes(const Plan& p) {
   return G;
 }
 
+// stream-K: the hand-off flags (zeroed before each launch, a 16-B multiple
+// at the region's start), then one BM x BN fp32 partial slot per block
+static size_t sk_flag_bytes(const Plan& p) { return ((size_t)p.sk_blocks * 4 + 15) / 16 * 16; }
 static size_t plan_ws(const Plan& p) {
+  if (p.sk) {
+    const TileCfg& t = kCfgs[p.tile - 2 * kNumCfgs];
+    return (sk_flag_bytes(p) + 255) / 256 * 256 + (size_t)p.sk_blocks * t.bm * t.bn * sizeof(float);
+  }
   return p.splits > 1 ? (size_t)p.splits * (size_t)p.M * (size_t)p.N * sizeof(float) : 0;
 }
 
@@ -850,35 +985,36 @@ static size_t stats_ws(int dtype, const Plan& p) {
 // Fast-path kernels (UT): FWD/DGRAD when the reduction channel radix is a
 // multiple of BK (every layer but conv1 FWD at BK = 16); WGRAD when BK / wo < ho
 // (one carry per radix and K-tile: the incremental pixel walk).
-template <int OP, int C, int DBG, bool X8>
+template <int OP, int C, int DBG, bool X8, bool SK>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t s) {
   constexpr TileCfg t = kCfgs[C];
   const bool fast = OP == OP_WGRAD ? t.bk / a.wo < a.ho : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
   if (fast) {
-    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, X8, DBG>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, X8, DBG, SK>), grid, dim3(256), 0, s, a);
     return;
   }
   if constexpr (DBG == 0)
-    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, X8, 0>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, X8, 0, SK>), grid, dim3(256), 0, s, a);
 }
 
-template <int OP, int DBG = 0, bool X8 = false>
+// SK: the stream-K grid (k_conv SK) of the tile
+template <int OP, int DBG = 0, bool X8 = false, bool SK = false>
 static void launch_op(int cfg, const ConvArgs& a, dim3 grid, hipStream_t s) {
   switch (cfg) {
-    case 0: launch_cfg<OP, 0, DBG, X8>(a, grid, s); break;
-    case 1: launch_cfg<OP, 1, DBG, X8>(a, grid, s); break;
-    case 2: launch_cfg<OP, 2, DBG, X8>(a, grid, s); break;
-    case 3: launch_cfg<OP, 3, DBG, X8>(a, grid, s); break;
-    case 4: launch_cfg<OP, 4, DBG, X8>(a, grid, s); break;
-    case 5: launch_cfg<OP, 5, DBG, X8>(a, grid, s); break;
-    case 6: launch_cfg<OP, 6, DBG, X8>(a, grid, s); break;
-    case 7: launch_cfg<OP, 7, DBG, X8>(a, grid, s); break;
-    case 8: launch_cfg<OP, 8, DBG, X8>(a, grid, s); break;
-    case 9: launch_cfg<OP, 9, DBG, X8>(a, grid, s); break;
-    case 10: launch_cfg<OP, 10, DBG, X8>(a, grid, s); break;
-    case 11: launch_cfg<OP, 11, DBG, X8>(a, grid, s); break;
-    case 12: launch_cfg<OP, 12, DBG, X8>(a, grid, s); break;
-    default: launch_cfg<OP, 13, DBG, X8>(a, grid, s); break;
+    case 0: launch_cfg<OP, 0, DBG, X8, SK>(a, grid, s); break;
+    case 1: launch_cfg<OP, 1, DBG, X8, SK>(a, grid, s); break;
+    case 2: launch_cfg<OP, 2, DBG, X8, SK>(a, grid, s); break;
+    case 3: launch_cfg<OP, 3, DBG, X8, SK>(a, grid, s); break;
+    case 4: launch_cfg<OP, 4, DBG, X8, SK>(a, grid, s); break;
+    case 5: launch_cfg<OP, 5, DBG, X8, SK>(a, grid, s); break;
+    case 6: launch_cfg<OP, 6, DBG, X8, SK>(a, grid, s); break;
+    case 7: launch_cfg<OP, 7, DBG, X8, SK>(a, grid, s); break;
+    case 8: launch_cfg<OP, 8, DBG, X8, SK>(a, grid, s); break;
+    case 9: launch_cfg<OP, 9, DBG, X8, SK>(a, grid, s); break;
+    case 10: launch_cfg<OP, 10, DBG, X8, SK>(a, grid, s); break;
+    case 11: launch_cfg<OP, 11, DBG, X8, SK>(a, grid, s); break;
+    case 12: launch_cfg<OP, 12, DBG, X8, SK>(a, grid, s); break;
+    default: launch_cfg<OP, 13, DBG, X8, SK>(a, grid, s); break;
   }
 }
 
@@ -977,6 +1113,19 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     a.c_mb = a.o_mb;
   }
   dim3 grid(p.mt * p.nt, members, p.splits);
+  if (p.sk) {
+    if (!ws || ws_bytes < plan_ws(p) + (members > 1 ? (size_t)(members - 1) * wsm : 0))
+      return fail(JR_ERR_WORKSPACE, "conv: workspace too small for the stream-K hand-off");
+    a.sk_ipb = p.sk_ipb;
+    a.sk_flags = static_cast<unsigned*>(ws);
+    a.sk_part = reinterpret_cast<float*>(static_cast<char*>(ws) + (sk_flag_bytes(p) + 255) / 256 * 256);
+    a.sk_mb = (long long)wsm;
+    grid = dim3(p.sk_blocks, members, 1);
+    // every polled word zeroed before EVERY launch (a memset node on the stream)
+    const hipError_t e = members > 1 ? hipMemset2DAsync(ws, wsm, 0, sk_flag_bytes(p), members, s)
+                                     : hipMemsetAsync(ws, 0, sk_flag_bytes(p), s);
+    if (e != hipSuccess) return fail(JR_ERR_HIP, "conv: stream-K flag reset failed");
+  }
   if (is_halo(dtype, p.tile)) {
     const HaloCfg& h = kHaloBf16[p.tile - kNumCfgsBf16];
     a.halo_wp = a.w + a.kw - 1;
@@ -1002,6 +1151,8 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
       launch_conv_bf16(OP, p.tile, am, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
   } else if (is_x8_f32(dtype, p.tile)) {
     launch_op<OP>(p.tile - kNumCfgs, a, grid, s);     // the fp32-MFMA kernel of that tile
+  } else if (p.sk) {
+    launch_op<OP, 0, true, true>(p.tile - 2 * kNumCfgs, a, grid, s);   // the stream-K grid of that x8 tile
   } else if (dtype == JR_F32_X8) {
     launch_op<OP, 0, true>(p.tile, a, grid, s);
   } else {

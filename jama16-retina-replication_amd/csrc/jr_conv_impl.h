@@ -46,6 +46,12 @@ struct ConvArgs {
   // members of A, B, C (the output, or the member's split-K slab region),
   // the statistics partials and the final output (split-K reduce)
   long long a_mb, b_mb, c_mb, s_mb, o_mb;
+  // stream-K (jr_conv.hip k_conv SK): iterations (tile-major, K-tile-minor)
+  // per block, the per-block hand-off flags (zeroed before every launch)
+  // and partial-tile slots; sk_mb = their member stride (grouped launches)
+  long long sk_ipb, sk_mb;
+  unsigned* sk_flags;
+  float* sk_part;
 };
 
 // Moves a grouped GEMM's operand / output pointers to member blockIdx.y
@@ -57,6 +63,10 @@ __device__ __forceinline__ void member_offsets(ConvArgs& g) {
     g.B = reinterpret_cast<const float*>(reinterpret_cast<const char*>(g.B) + m * g.b_mb);
     g.C = reinterpret_cast<float*>(reinterpret_cast<char*>(g.C) + m * g.c_mb);
     if (g.stats) g.stats = reinterpret_cast<float*>(reinterpret_cast<char*>(g.stats) + m * g.s_mb);
+    if (g.sk_flags) {
+      g.sk_flags = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(g.sk_flags) + m * g.sk_mb);
+      g.sk_part = reinterpret_cast<float*>(reinterpret_cast<char*>(g.sk_part) + m * g.sk_mb);
+    }
   }
 }
 

@@ -56,10 +56,12 @@ def test_validation_errors_without_gpu():
     assert L.jr_conv2d_workspace_size(None, 0, 0) == 0
     # JR_F32_X8 (dtype 2): fp32 storage rules and tile table, conv entry points only
     d = _ffi.ConvDesc(2, 17, 17, 64, 96, 3, 3, 1, 1, 1, 1, 17, 17, 0, 64, 0, 96)
-    # (x8 ids 0-13: the split kernel; 14-27: the fp32-MFMA kernel of the same tiles)
-    assert L.jr_conv2d_num_configs(2) == 2 * L.jr_conv2d_num_configs(0) > 0
+    # (x8 ids 0-13: the split kernel; 14-27: the fp32-MFMA kernel of the same
+    # tiles; 28-41: the stream-K grid of the split kernel, whose hand-off slots
+    # need more workspace)
+    assert L.jr_conv2d_num_configs(2) == 3 * L.jr_conv2d_num_configs(0) > 0
     for op in range(3):
-        assert L.jr_conv2d_workspace_size(ctypes.byref(d), op, 2) == L.jr_conv2d_workspace_size(ctypes.byref(d), op, 0)
+        assert L.jr_conv2d_workspace_size(ctypes.byref(d), op, 2) >= L.jr_conv2d_workspace_size(ctypes.byref(d), op, 0)
     # JR_F32_X8P (dtype 3): bf16-operand channel rules (radix 8), its own tile table
     assert L.jr_conv2d_num_configs(3) > 0
     assert L.jr_conv2d_workspace_size(ctypes.byref(d), 0, 3) > 0

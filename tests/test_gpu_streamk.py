@@ -1,0 +1,166 @@
+"""Stream-K x8 convolutions (JR_F32_X8 ids 28..41: the stream-K grid of x8
+tile id - 28, k_conv SK in csrc/jr_conv.hip).
+
+A fixed grid of blocks walks equal ranges of the GEMM's tiles x K-tiles; a
+tile cut between blocks is finished by the block holding its first K-tile,
+which adds the later pieces' fp32 partials (published write-through, behind
+an agent-scope flag) in block order.  Checked here:
+  * fwd (with the fused BN statistics), dgrad (every stride phase,
+    accumulate) and wgrad against the fp64 oracle at the fp32 bars of
+    test_gpu_ops.py (5e-6 / 1e-5 of max|ref|), on geometries whose tiles are
+    cut into 2, 3 and 30+ pieces (the deep chains of a one-tile-row GEMM);
+  * determinism: two runs are bitwise equal (fixed cut points, fixed order);
+  * grouped (ensemble members) stream-K: bitwise the per-member call.
+Every other x8 id (and the stream-K ids on small shapes) is covered by
+test_gpu_ops.py::test_conv_every_tile_config.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import tf_ops as R
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+X8, SK0 = 2, 28
+_KEEP = []
+
+
+@pytest.fixture(autouse=True)
+def _keep_alive():
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
+
+
+def _lib():
+    from jr import _ffi
+    _ffi.init(0)
+    return _ffi
+
+
+def dev(a):
+    t = torch.as_tensor(np.ascontiguousarray(a)).to("cuda")
+    _KEEP.append(t)
+    return t
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def relerr(got, ref):
+    ref = np.asarray(ref, np.float64)
+    return float(np.max(np.abs(got - ref)) / max(np.max(np.abs(ref)), 1e-30))
+
+
+CASES = [
+    (4, 17, 17, 192, 192, 1, 7, 1, "same"),     # 17^2 1x7: tiles cut in 2-3 pieces
+    (4, 35, 35, 96, 96, 3, 3, 1, "same"),       # 35^2 3x3
+    (2, 35, 35, 288, 384, 3, 3, 2, "valid"),    # stride 2: four dgrad phases
+    (4, 8, 8, 2048, 384, 1, 1, 1, "same"),      # one tile row, K = 2048: 30+ pieces per tile
+    (2, 37, 37, 3, 32, 3, 3, 2, "valid"),       # conv1 geometry (generic address path)
+]
+
+
+def _set(ffi, L, d, s, cin, cfg):
+    for op in (0, 2):
+        ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), op, X8, 0, cfg))
+    if cin % 4 == 0:
+        for ph in range(s * s):
+            ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 1, X8, ph, cfg))
+
+
+@pytest.mark.parametrize("tile", [11, 12, 13, 3, 1])
+@pytest.mark.parametrize("case", CASES)
+def test_stream_k_matches_oracle_and_is_deterministic(case, tile):
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, cin, cout, kh, kw, s, pad = case
+    rng = np.random.default_rng(hash((case, tile)) % 2**31)
+    x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
+    wt = (rng.standard_normal((kh, kw, cin, cout)) / np.sqrt(kh * kw * cin)).astype(np.float32)
+    cs = (cin + 3) // 4 * 4
+    xp = np.zeros((n, h, w, cs), np.float32)
+    xp[..., :cin] = x
+    ph, pw = ((kh - 1) // 2, (kw - 1) // 2) if pad == "same" else (0, 0)
+    ho, wo = (h + 2 * ph - kh) // s + 1, (w + 2 * pw - kw) // s + 1
+    d = ffi.ConvDesc(n, h, w, cin, cout, kh, kw, s, s, ph, pw, ho, wo, 0, cs, 0, cout)
+    ref = R.conv2d(x, wt, s, pad)
+    dy = rng.standard_normal(ref.shape).astype(np.float32)
+    X, W, DY = dev(xp), dev(wt), dev(dy)
+    _set(ffi, L, d, s, cin, SK0 + tile)
+    try:
+        wsb = max(L.jr_conv2d_workspace_size(ctypes.byref(d), op, X8) for op in range(3))
+        ws = torch.zeros(wsb // 4 + 4, device="cuda")
+        outs = []
+        for rep in range(2):
+            Y = torch.zeros(ref.size, device="cuda")
+            st = torch.zeros(2 * cout, device="cuda")
+            ffi.check("fwd", L.jr_conv2d_fwd_bn_stats(ctypes.byref(d), X8, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
+                                                      1e-3, st.data_ptr(), st.data_ptr() + 4 * cout, ws.data_ptr(),
+                                                      wsb, None))
+            DW = torch.zeros(wt.size, device="cuda")
+            ffi.check("wgrad", L.jr_conv2d_bwd_filter(ctypes.byref(d), X8, X.data_ptr(), DY.data_ptr(),
+                                                      DW.data_ptr(), ws.data_ptr(), wsb, None))
+            o = [host(Y), host(st), host(DW)]
+            if cin % 4 == 0:
+                DX = torch.zeros(xp.size, device="cuda")
+                ffi.check("dgrad", L.jr_conv2d_bwd_data(ctypes.byref(d), X8, DY.data_ptr(), W.data_ptr(),
+                                                        DX.data_ptr(), 0, ws.data_ptr(), wsb, None))
+                o.append(host(DX))
+                ffi.check("dgrad acc", L.jr_conv2d_bwd_data(ctypes.byref(d), X8, DY.data_ptr(), W.data_ptr(),
+                                                            DX.data_ptr(), 1, ws.data_ptr(), wsb, None))
+                o.append(host(DX))
+            outs.append(o)
+    finally:
+        _set(ffi, L, d, s, cin, -1)
+    y, st, dw = outs[0][:3]
+    assert relerr(y.reshape(ref.shape), ref) < 5e-6
+    mean = ref.reshape(-1, cout).mean(0)
+    var = ref.reshape(-1, cout).var(0)
+    assert np.max(np.abs(st[:cout] - mean)) <= 1e-5 * np.abs(ref).max()
+    assert np.max(np.abs(st[cout:] * np.sqrt(var + 1e-3) - 1)) < 1e-5
+    assert relerr(dw.reshape(wt.shape), R.conv2d_bwd_filter(x, dy, wt.shape, s, pad)) < 1e-5
+    if cin % 4 == 0:
+        ref_dx = R.conv2d_bwd_data(dy, wt, x.shape, s, pad)
+        assert relerr(outs[0][3].reshape(n, h, w, cs)[..., :cin], ref_dx) < 5e-6
+        assert relerr(outs[0][4].reshape(n, h, w, cs)[..., :cin], 2 * ref_dx) < 5e-6
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)                      # bitwise reproducible
+
+
+def test_stream_k_grouped_members():
+    """Ensemble members through one grouped stream-K launch per GEMM: bitwise
+    the per-member stream-K call (the same cut points per member)."""
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, cin, cout, kh, kw = 4, 17, 17, 192, 192, 1, 7
+    d = ffi.ConvDesc(n, h, w, cin, cout, kh, kw, 1, 1, 0, 3, h, w, 0, cin, 0, cout)
+    M = 3
+    g = torch.Generator(device="cuda").manual_seed(9)
+    xm, wm, ym = n * h * w * cin, kh * kw * cin * cout, n * h * w * cout
+    X = torch.randn(M * xm, device="cuda", generator=g)
+    W = torch.randn(M * wm, device="cuda", generator=g) * 0.05
+    ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, X8, 0, SK0 + 11))
+    try:
+        wsb = L.jr_conv2d_workspace_size_grouped(ctypes.byref(d), X8, M)
+        ws = torch.zeros(wsb // 4 + 4, device="cuda")
+        Yg, Sg = torch.zeros(M * ym, device="cuda"), torch.zeros(M * 2 * cout, device="cuda")
+        ffi.check("grouped", L.jr_conv2d_fwd_bn_stats_grouped(
+            ctypes.byref(d), X8, M, X.data_ptr(), xm, W.data_ptr(), wm, Yg.data_ptr(), ym, 1e-3, Sg.data_ptr(),
+            Sg.data_ptr() + 4 * cout, 2 * cout, ws.data_ptr(), wsb, None))
+        ws1 = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, X8)
+        w1 = torch.zeros(ws1 // 4 + 4, device="cuda")
+        for m in range(M):
+            Y, S = torch.zeros(ym, device="cuda"), torch.zeros(2 * cout, device="cuda")
+            ffi.check("single", L.jr_conv2d_fwd_bn_stats(
+                ctypes.byref(d), X8, X.data_ptr() + 4 * m * xm, W.data_ptr() + 4 * m * wm, Y.data_ptr(), 1e-3,
+                S.data_ptr(), S.data_ptr() + 4 * cout, w1.data_ptr(), ws1, None))
+            torch.cuda.synchronize()
+            assert torch.equal(Yg[m * ym:(m + 1) * ym], Y) and torch.equal(Sg[m * 2 * cout:(m + 1) * 2 * cout], S)
+    finally:
+        ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, X8, 0, -1))
