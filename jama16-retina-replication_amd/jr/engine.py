@@ -48,7 +48,9 @@ def pinned_tile_table(conv_math: str, batch: int, height: int, width: int, train
     """The committed tile table (jr/tiles_mi355x.json) of this workload, or None."""
     global _PINNED
     if _PINNED is None:
-        p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tiles_mi355x.json")
+        # (JR_TILE_TABLES: another table file, for A/B runs of re-tuned tables)
+        p = os.environ.get("JR_TILE_TABLES") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                             "tiles_mi355x.json")
         _PINNED = json.load(open(p))["tables"] if os.path.exists(p) else []
     for t in _PINNED:
         if (t["conv_math"], t["batch"], t["height"], t["width"], t["train"]) == (conv_math, batch, height, width,
