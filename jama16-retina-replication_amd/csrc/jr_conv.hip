@@ -864,9 +864,11 @@ static Plan plan_with(int dtype, int cfg, int M, int N, int K) {
   if (is_sk(dtype, p.tile)) {
     // stream-K: a fixed grid (two blocks per CU at most resident; larger
     // tiles run it in two equal rounds), at least kSkMinIters K-tiles each
+    // (the config's split field picks the grid instead: 128 x s blocks, s <= 8)
+    const long long grid = cfg_splits(cfg) > 0 ? 128LL * std::min(cfg_splits(cfg), 8) : kSkBlocks;
     splits = 1;
     const long long W = (long long)tiles * std::max(p.ktiles, 1);
-    const long long P = std::max(1LL, std::min<long long>(kSkBlocks, W / kSkMinIters));
+    const long long P = std::max(1LL, std::min<long long>(grid, W / kSkMinIters));
     p.sk = true;
     p.sk_ipb = ceil_div(W, P);
     p.sk_blocks = (int)ceil_div(W, p.sk_ipb);
@@ -1365,6 +1367,13 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
       if (c < 0) break;
       tile_t[c] = 1e30f;
       const Plan dp = plan_with(dtype, c, M, N, K);
+      if (dp.sk) {   // stream-K: other grid sizes (128 x v blocks) instead of split factors
+        for (int v : {2, 3, 6, 8}) {
+          time_cfg(c | (v << kSplitShift));
+          if (rc) break;
+        }
+        continue;
+      }
       int prev = -1;
       for (int v : {1, dp.splits / 4, dp.splits / 2, dp.splits * 2}) {
         if (v < 1 || v == dp.splits || v == prev || v > kMaxSplits || v > dp.ktiles) continue;
