@@ -41,6 +41,7 @@
 #include <type_traits>
 #include <map>
 #include <mutex>
+#include <vector>
 
 namespace jr {
 
@@ -144,66 +145,6 @@ struct SplitFrag {
 // its ordinary epilogue (store + fused BN statistics).  Waits point only to
 // higher blocks, which publish before waiting on anything, so no block waits
 // on one that cannot start; spins are bounded.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sk_rsrc(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
-}
-
-template <int TM, int TN>
-__device__ __forceinline__ void sk_publish(const ConvArgs& g, const f32x16 (&acc)[TM][TN], int wave, int lane) {
-  constexpr int SLOT = 4 * TM * TN * 16 * 64;               // floats per block slot (BM x BN)
-  const auto rs = sk_rsrc(g.sk_part + (long long)blockIdx.x * SLOT);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        typedef int i32x4 __attribute__((ext_vector_type(4)));
-        const i32x4 v = {__float_as_int(acc[i][j][4 * q]), __float_as_int(acc[i][j][4 * q + 1]),
-                         __float_as_int(acc[i][j][4 * q + 2]), __float_as_int(acc[i][j][4 * q + 3])};
-        const int off = (((((wave * TM + i) * TN + j) * 4 + q) * 64) + lane) * 16;
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);    // aux 16 = sc1 (write-through)
-      }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // every storing wave drains
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store(g.sk_flags + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// acc += the partial of block b (published by sk_publish), after its flag
-template <int TM, int TN>
-__device__ __forceinline__ void sk_absorb(const ConvArgs& g, f32x16 (&acc)[TM][TN], int b, int wave, int lane) {
-  constexpr int SLOT = 4 * TM * TN * 16 * 64;
-  if (threadIdx.x == 0) {            // ONE lane polls ONE word, relaxed; bounded (~1 s), then gives up
-    for (unsigned spins = 0; spins < (1u << 22); ++spins) {
-      if (__hip_atomic_load(g.sk_flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below the poll)
-  const auto rs = sk_rsrc(g.sk_part + (long long)b * SLOT);
-  typedef int i32x4 __attribute__((ext_vector_type(4)));
-  // one accumulator row i at a time (TN x 4 loads in flight): the loaded
-  // partial never holds more than TN x 16 VGPRs
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    i32x4 v[TN][4];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)   // every load of the hand-off sc1 (write-through producer, drained)
-        v[j][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (((((wave * TM + i) * TN + j) * 4 + q) * 64) + lane) * 16,
-                                                        0, 16);
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += __int_as_float(v[j][q][e]);
-  }
-}
-
 template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0, bool SK = false>
 __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int WGN = 4 / WGM;
@@ -769,6 +710,7 @@ struct Plan {
   bool sk;
   int sk_blocks;
   long long sk_ipb;
+  int sk_slot;   // floats of one block's partial (BM x BN)
 };
 
 // Channel padding of the reduction operand: 16 B DMA pieces hold 4 fp32 or
@@ -789,28 +731,42 @@ static int std_count(int dtype) {
 // MFMA gain, the fp32 MFMA is the faster one -- autotuning and the pinned
 // tables choose per GEMM (the planner heuristic keeps x8).
 // JR_BF16 ids: [0, 17) GEMM tiles, [17, 25) halo configs, then the wide
-// (8-wave) tiles; JR_F32_X8P: [0, 17) tiles, then the wide ones (new ids are
-// appended so committed tile tables keep their meaning).
+// (8-wave) tiles, then the stream-K grids of the GEMM tiles and of the wide
+// tiles (k_conv_bf16 SK); JR_F32_X8P: [0, 17) tiles, then the wide ones (new
+// ids are appended so committed tile tables keep their meaning).
 static int wide_base(int dtype) {
   return dtype == JR_BF16 ? kNumCfgsBf16 + kNumHaloBf16 : dtype == JR_F32_X8P ? kNumCfgsX8P : 1 << 20;
 }
+static int wide_count(int dtype) {
+  return dtype == JR_BF16 ? kNumCfgsBf16W : dtype == JR_F32_X8P ? kNumCfgsX8PW : 0;
+}
+// first stream-K id: JR_F32_X8 [28, 42) = the stream-K grid of x8 tile
+// (id - 28) (k_conv SK); JR_BF16 see above
+static int sk_base(int dtype) {
+  return dtype == JR_F32_X8 ? 2 * kNumCfgs : dtype == JR_BF16 ? wide_base(dtype) + kNumCfgsBf16W : 1 << 20;
+}
 static int cfg_count(int dtype) {
-  return dtype == JR_BF16 ? wide_base(dtype) + kNumCfgsBf16W
+  return dtype == JR_BF16 ? sk_base(dtype) + kNumCfgsBf16 + kNumCfgsBf16W
          : dtype == JR_F32_X8P ? wide_base(dtype) + kNumCfgsX8PW
-         : std_count(dtype) + (dtype == JR_F32_X8 ? 2 * kNumCfgs : 0);
+         : dtype == JR_F32_X8 ? 3 * kNumCfgs
+         : std_count(dtype);
 }
 static bool is_halo(int dtype, int tile) {
   return dtype == JR_BF16 && tile >= kNumCfgsBf16 && tile < kNumCfgsBf16 + kNumHaloBf16;
 }
-static bool is_wide(int dtype, int tile) { return tile >= wide_base(dtype) && tile < cfg_count(dtype); }
+static bool is_wide(int dtype, int tile) { return tile >= wide_base(dtype) && tile < wide_base(dtype) + wide_count(dtype); }
 static bool is_x8_f32(int dtype, int tile) { return dtype == JR_F32_X8 && tile >= kNumCfgs && tile < 2 * kNumCfgs; }
-// JR_F32_X8 ids [28, 42): the stream-K grid of x8 tile (id - 28) (k_conv SK)
-static bool is_sk(int dtype, int tile) { return dtype == JR_F32_X8 && tile >= 2 * kNumCfgs; }
+static bool is_sk(int dtype, int tile) { return tile >= sk_base(dtype) && tile < cfg_count(dtype); }
+// the (non-stream-K) id whose tile a stream-K id runs
+static int sk_tile(int dtype, int tile) {
+  const int k = tile - sk_base(dtype);
+  return dtype == JR_BF16 && k >= kNumCfgsBf16 ? wide_base(dtype) + k - kNumCfgsBf16 : k;
+}
 static const TileCfg& tile_cfg(int dtype, int tile) {
+  if (is_sk(dtype, tile)) tile = sk_tile(dtype, tile);
   if (is_halo(dtype, tile)) return kHaloBf16[tile - kNumCfgsBf16].t;
   if (is_wide(dtype, tile)) return (dtype == JR_BF16 ? kCfgsBf16W : kCfgsX8PW)[tile - wide_base(dtype)];
   if (is_x8_f32(dtype, tile)) return kCfgs[tile - kNumCfgs];
-  if (is_sk(dtype, tile)) return kCfgs[tile - 2 * kNumCfgs];
   return (dtype == JR_BF16 ? kCfgsBf16 : dtype == JR_F32_X8P ? kCfgsX8P : kCfgs)[tile];
 }
 // Halo rows a BM-row tile needs: output rows it spans (bound) + kh - 1.
@@ -872,6 +828,7 @@ static Plan plan_with(int dtype, int cfg, int M, int N, int K) {
     p.sk = true;
     p.sk_ipb = ceil_div(W, P);
     p.sk_blocks = (int)ceil_div(W, p.sk_ipb);
+    p.sk_slot = t.bm * t.bn;
   }
   p.kt_per_split = (int)ceil_div(std::max(p.ktiles, 1), splits);
   p.splits = (int)ceil_div(std::max(p.ktiles, 1), p.kt_per_split);
@@ -940,10 +897,7 @@ static int reduce_lanes(const Plan& p) {
 // at the region's start), then one BM x BN fp32 partial slot per block
 static size_t sk_flag_bytes(const Plan& p) { return ((size_t)p.sk_blocks * 4 + 15) / 16 * 16; }
 static size_t plan_ws(const Plan& p) {
-  if (p.sk) {
-    const TileCfg& t = kCfgs[p.tile - 2 * kNumCfgs];
-    return (sk_flag_bytes(p) + 255) / 256 * 256 + (size_t)p.sk_blocks * t.bm * t.bn * sizeof(float);
-  }
+  if (p.sk) return (sk_flag_bytes(p) + 255) / 256 * 256 + (size_t)p.sk_blocks * p.sk_slot * sizeof(float);
   return p.splits > 1 ? (size_t)p.splits * (size_t)p.M * (size_t)p.N * sizeof(float) : 0;
 }
 
@@ -1147,7 +1101,11 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
       const int cred = OP == OP_FWD ? a.cp : a.cout;
       am = cred % t.bk == 0 ? 0 : cred >= t.bk ? 1 : 2;
     }
-    if (is_wide(dtype, p.tile))
+    if (p.sk) {   // the stream-K grid of a standard or wide JR_BF16 tile
+      const int tt = sk_tile(dtype, p.tile);
+      const bool w = is_wide(dtype, tt);
+      launch_conv_bf16_sk(OP, w ? tt - wide_base(dtype) : tt, w, am, a, grid, s);
+    } else if (is_wide(dtype, p.tile))
       launch_conv_bf16_wide(OP, p.tile - wide_base(dtype), am, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
     else
       launch_conv_bf16(OP, p.tile, am, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
@@ -1357,7 +1315,7 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
       return ms;
     };
     // pass 1: every tile with the planner's split-K factor
-    float tile_t[64];
+    std::vector<float> tile_t(ncfg);
     for (int c = 0; c < ncfg && !rc; ++c) tile_t[c] = time_cfg(c);
     // pass 2: the three fastest tiles with other split-K factors
     for (int pick = 0; pick < 3 && !rc; ++pick) {

@@ -43,7 +43,10 @@ __device__ __forceinline__ s16x4 lds_tr(const uint16_t* p) {
 // DGRAD with cred % BK == 0), 1 = incremental per-lane walk (one carry per
 // radix per K-tile), 2 = mixed-radix loop (conv1's 8 padded channels, tiny
 // images).
-template <int OP, int BM, int BN, int WGM, int BK, int NBUF, int AM, int NP, int NW>
+// SK: the stream-K grid (the scheme of jr_conv.hip k_conv SK: equal ranges of
+// tiles x K-tiles per block, cut tiles finished by the block holding their
+// first K-tile from the later pieces' write-through partials).
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, int AM, int NP, int NW, bool SK = false>
 __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
   static_assert(NP == 1 || NP == 3, "one bf16 plane, or the h / m / l planes of X8P");
   static_assert(NW == 4 || NW == 8, "4 or 8 waves per block");
@@ -76,11 +79,30 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
   const int wm0 = (wave / WGN) * WM;
   const int wn0 = (wave % WGN) * WN;
 
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  long long sk_it = 0, sk_end = 0;
+  if constexpr (SK) {
+    const long long W = (long long)((g.M + BM - 1) / BM) * g.ntn * g.ktiles;
+    sk_it = (long long)blockIdx.x * g.sk_ipb;
+    sk_end = sk_it + g.sk_ipb < W ? sk_it + g.sk_ipb : W;
+  }
+  bool sk_first = true;
+  // one iteration per (tile, K range) segment: ordinary launches run exactly one
+  for (;;) {
+  int tile, kt0, kt1;
+  if constexpr (SK) {
+    if (sk_it >= sk_end) break;
+    tile = (int)(sk_it / g.ktiles);
+    kt0 = (int)(sk_it - (long long)tile * g.ktiles);
+    kt1 = (int)(sk_end - sk_it < (long long)(g.ktiles - kt0) ? kt0 + (sk_end - sk_it) : g.ktiles);
+    sk_it += kt1 - kt0;
+    if (!sk_first) __syncthreads();      // the previous segment's stage / ring reads are done
+  } else {
+    tile = xcd_remap(blockIdx.x, gridDim.x);
+    kt0 = blockIdx.z * g.kt_per_split;
+    kt1 = min(g.ktiles, kt0 + g.kt_per_split);
+  }
   const int mt = tile / g.ntn, nt = tile - mt * g.ntn;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int kt0 = blockIdx.z * g.kt_per_split;
-  const int kt1 = min(g.ktiles, kt0 + g.kt_per_split);
   // the zero page's address lives in an SGPR pair for the whole kernel (hipcc
   // otherwise rematerialises it with s_getpc + two v_mov per DMA piece)
   unsigned long long zpa = reinterpret_cast<unsigned long long>(g_zero_page);
@@ -491,71 +513,84 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
   }
   JR_ST(stamp.loop();)
 
+  if constexpr (SK) {
+    const bool first = sk_first;
+    sk_first = false;
+    if (kt0 != 0) {                  // (only a block's first segment starts inside a tile)
+      if (first) sk_publish<TM, TN, NW>(g, acc, wave, lane);
+      continue;
+    }
+    for (int b = blockIdx.x + 1, covered = kt1; covered < g.ktiles; ++b, covered += (int)g.sk_ipb)
+      sk_absorb<TM, TN, NW>(g, acc, b, wave, lane);
+  }
   // ---------------------------------------------------------------- epilogue
   conv_epilogue<OP, WM, TM, TN, NP == 1>(g, acc, reinterpret_cast<float*>(smem) + wave * stage_floats<WN>(), m0 + wm0,
                                       n0 + wn0, lane);
+  if constexpr (!SK) break;
+  }
   JR_ST(stamp.end(g.dbg);)
 }
 
-template <int OP, int NP, int BM, int BN, int WGM, int BK, int NBUF, int NW>
+template <int OP, int NP, int BM, int BN, int WGM, int BK, int NBUF, int NW, bool SK>
 static void launch_cfg_t(int am, const ConvArgs& a, dim3 grid, hipStream_t s) {
   if constexpr (OP != OP_WGRAD) {
     if (am == 0) {
-      hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, 0, NP, NW>), grid, dim3(64 * NW), 0, s, a);
+      hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, 0, NP, NW, SK>), grid, dim3(64 * NW), 0, s, a);
       return;
     }
   }
   if (am == 1)
-    hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, 1, NP, NW>), grid, dim3(64 * NW), 0, s, a);
+    hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, 1, NP, NW, SK>), grid, dim3(64 * NW), 0, s, a);
   else
-    hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, 2, NP, NW>), grid, dim3(64 * NW), 0, s, a);
+    hipLaunchKernelGGL((k_conv_bf16<OP, BM, BN, WGM, BK, NBUF, 2, NP, NW, SK>), grid, dim3(64 * NW), 0, s, a);
 }
 
-// config c of the standard (W = false) or wide (W = true) table of NP
-template <int OP, int C, int NP, bool W>
+// config c of the standard (W = false) or wide (W = true) table of NP; SK:
+// its stream-K grid (JR_BF16 only)
+template <int OP, int C, int NP, bool W, bool SK>
 static void launch_tile(int am, const ConvArgs& a, dim3 grid, hipStream_t s) {
   if constexpr (W) {
     constexpr int n = NP == 1 ? kNumCfgsBf16W : kNumCfgsX8PW;
     if constexpr (C < n) {
       constexpr TileCfg t = NP == 1 ? kCfgsBf16W[C] : kCfgsX8PW[C];
-      launch_cfg_t<OP, NP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, t.nw>(am, a, grid, s);
+      launch_cfg_t<OP, NP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, t.nw, SK>(am, a, grid, s);
     }
   } else {
     constexpr TileCfg t = NP == 1 ? kCfgsBf16[C] : kCfgsX8P[C];
-    launch_cfg_t<OP, NP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, t.nw>(am, a, grid, s);
+    launch_cfg_t<OP, NP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, t.nw, SK>(am, a, grid, s);
   }
 }
 
-template <int OP, int NP, bool W>
+template <int OP, int NP, bool W, bool SK = false>
 static void launch_op_bf16(int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s) {
   static_assert(kNumCfgsBf16 == 17 && kNumCfgsX8P == 17, "keep the switch in sync with kCfgsBf16 / kCfgsX8P");
   static_assert(kNumCfgsBf16W <= 17 && kNumCfgsX8PW <= 17, "keep the switch in sync with the wide tables");
   switch (tile) {
-    case 0: launch_tile<OP, 0, NP, W>(am, a, grid, s); break;
-    case 1: launch_tile<OP, 1, NP, W>(am, a, grid, s); break;
-    case 2: launch_tile<OP, 2, NP, W>(am, a, grid, s); break;
-    case 3: launch_tile<OP, 3, NP, W>(am, a, grid, s); break;
-    case 4: launch_tile<OP, 4, NP, W>(am, a, grid, s); break;
-    case 5: launch_tile<OP, 5, NP, W>(am, a, grid, s); break;
-    case 6: launch_tile<OP, 6, NP, W>(am, a, grid, s); break;
-    case 7: launch_tile<OP, 7, NP, W>(am, a, grid, s); break;
-    case 8: launch_tile<OP, 8, NP, W>(am, a, grid, s); break;
-    case 9: launch_tile<OP, 9, NP, W>(am, a, grid, s); break;
-    case 10: launch_tile<OP, 10, NP, W>(am, a, grid, s); break;
-    case 11: launch_tile<OP, 11, NP, W>(am, a, grid, s); break;
-    case 12: launch_tile<OP, 12, NP, W>(am, a, grid, s); break;
-    case 13: launch_tile<OP, 13, NP, W>(am, a, grid, s); break;
-    case 14: launch_tile<OP, 14, NP, W>(am, a, grid, s); break;
-    case 15: launch_tile<OP, 15, NP, W>(am, a, grid, s); break;
-    default: launch_tile<OP, 16, NP, W>(am, a, grid, s); break;
+    case 0: launch_tile<OP, 0, NP, W, SK>(am, a, grid, s); break;
+    case 1: launch_tile<OP, 1, NP, W, SK>(am, a, grid, s); break;
+    case 2: launch_tile<OP, 2, NP, W, SK>(am, a, grid, s); break;
+    case 3: launch_tile<OP, 3, NP, W, SK>(am, a, grid, s); break;
+    case 4: launch_tile<OP, 4, NP, W, SK>(am, a, grid, s); break;
+    case 5: launch_tile<OP, 5, NP, W, SK>(am, a, grid, s); break;
+    case 6: launch_tile<OP, 6, NP, W, SK>(am, a, grid, s); break;
+    case 7: launch_tile<OP, 7, NP, W, SK>(am, a, grid, s); break;
+    case 8: launch_tile<OP, 8, NP, W, SK>(am, a, grid, s); break;
+    case 9: launch_tile<OP, 9, NP, W, SK>(am, a, grid, s); break;
+    case 10: launch_tile<OP, 10, NP, W, SK>(am, a, grid, s); break;
+    case 11: launch_tile<OP, 11, NP, W, SK>(am, a, grid, s); break;
+    case 12: launch_tile<OP, 12, NP, W, SK>(am, a, grid, s); break;
+    case 13: launch_tile<OP, 13, NP, W, SK>(am, a, grid, s); break;
+    case 14: launch_tile<OP, 14, NP, W, SK>(am, a, grid, s); break;
+    case 15: launch_tile<OP, 15, NP, W, SK>(am, a, grid, s); break;
+    default: launch_tile<OP, 16, NP, W, SK>(am, a, grid, s); break;
   }
 }
 
-template <int NP, bool W>
+template <int NP, bool W, bool SK = false>
 static void launch_np(int op, int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s) {
-  if (op == OP_FWD) launch_op_bf16<OP_FWD, NP, W>(tile, am, a, grid, s);
-  else if (op == OP_DGRAD) launch_op_bf16<OP_DGRAD, NP, W>(tile, am, a, grid, s);
-  else launch_op_bf16<OP_WGRAD, NP, W>(tile, am, a, grid, s);
+  if (op == OP_FWD) launch_op_bf16<OP_FWD, NP, W, SK>(tile, am, a, grid, s);
+  else if (op == OP_DGRAD) launch_op_bf16<OP_DGRAD, NP, W, SK>(tile, am, a, grid, s);
+  else launch_op_bf16<OP_WGRAD, NP, W, SK>(tile, am, a, grid, s);
 }
 
 void launch_conv_bf16(int op, int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s, int np) {
@@ -566,6 +601,11 @@ void launch_conv_bf16(int op, int tile, int am, const ConvArgs& a, dim3 grid, hi
 void launch_conv_bf16_wide(int op, int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s, int np) {
   if (np == 3) launch_np<3, true>(op, tile, am, a, grid, s);
   else launch_np<1, true>(op, tile, am, a, grid, s);
+}
+
+void launch_conv_bf16_sk(int op, int tile, bool wide, int am, const ConvArgs& a, dim3 grid, hipStream_t s) {
+  if (wide) launch_np<1, true, true>(op, tile, am, a, grid, s);
+  else launch_np<1, false, true>(op, tile, am, a, grid, s);
 }
 
 }  // namespace jr

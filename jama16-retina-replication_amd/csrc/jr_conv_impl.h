@@ -164,6 +164,71 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_chunk) {
                                    (__attribute__((address_space(3))) void*)lds_chunk, 16, 0, 0);
 }
 
+// ---------------------------------------------------------------- stream-K
+// Hand-off of a cut tile's later pieces (jr_conv.hip k_conv SK documents the
+// scheme; k_conv_bf16 uses the same): write-through partials + one flag per
+// block, the owner's relaxed poll and sc1 loads.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sk_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+template <int TM, int TN, int NW = 4>
+__device__ __forceinline__ void sk_publish(const ConvArgs& g, const f32x16 (&acc)[TM][TN], int wave, int lane) {
+  constexpr int SLOT = NW * TM * TN * 16 * 64;              // floats per block slot (BM x BN)
+  const auto rs = sk_rsrc(g.sk_part + (long long)blockIdx.x * SLOT);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const i32x4 v = {__float_as_int(acc[i][j][4 * q]), __float_as_int(acc[i][j][4 * q + 1]),
+                         __float_as_int(acc[i][j][4 * q + 2]), __float_as_int(acc[i][j][4 * q + 3])};
+        const int off = (((((wave * TM + i) * TN + j) * 4 + q) * 64) + lane) * 16;
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);    // aux 16 = sc1 (write-through)
+      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(g.sk_flags + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// acc += the partial of block b (published by sk_publish), after its flag
+template <int TM, int TN, int NW = 4>
+__device__ __forceinline__ void sk_absorb(const ConvArgs& g, f32x16 (&acc)[TM][TN], int b, int wave, int lane) {
+  constexpr int SLOT = NW * TM * TN * 16 * 64;
+  if (threadIdx.x == 0) {            // ONE lane polls ONE word, relaxed; bounded (~1 s), then gives up
+    for (unsigned spins = 0; spins < (1u << 22); ++spins) {
+      if (__hip_atomic_load(g.sk_flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below the poll)
+  const auto rs = sk_rsrc(g.sk_part + (long long)b * SLOT);
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  // one accumulator row i at a time (TN x 4 loads in flight): the loaded
+  // partial never holds more than TN x 16 VGPRs
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    i32x4 v[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)   // every load of the hand-off sc1 (write-through producer, drained)
+        v[j][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (((((wave * TM + i) * TN + j) * 4 + q) * 64) + lane) * 16,
+                                                        0, 16);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += __int_as_float(v[j][q][e]);
+  }
+}
+
+
 // ---------------------------------------------------------------- epilogue
 // A wave's WM x WN accumulator tile leaves 32 rows at a time through the
 // wave's own LDS region [32][WN + 8] fp32 (the two 32-lane halves of a store
@@ -631,5 +696,7 @@ void launch_conv_halo(int h, const ConvArgs& a, dim3 grid, hipStream_t s);
 void launch_conv_bf16(int op, int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s, int np = 1);
 // the same kernel on a wide tile: index into kCfgsBf16W (np = 1) / kCfgsX8PW (np = 3)
 void launch_conv_bf16_wide(int op, int tile, int am, const ConvArgs& a, dim3 grid, hipStream_t s, int np = 1);
+// the stream-K grid of a JR_BF16 tile (standard, or wide with wide = true)
+void launch_conv_bf16_sk(int op, int tile, bool wide, int am, const ConvArgs& a, dim3 grid, hipStream_t s);
 
 }  // namespace jr

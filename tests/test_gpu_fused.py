@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 _KEEP = []
-WIDE_BF16 = 8          # jr_conv_impl.h kCfgsBf16W: the last config ids of JR_BF16
+WIDE0_BF16 = 25        # jr_conv_impl.h kCfgsBf16W: JR_BF16 ids after the 17 tiles and 8 halo configs
 
 
 @pytest.fixture(autouse=True)
@@ -83,7 +83,7 @@ def test_conv_fwd_bn_stats(case, dtype):
     _KEEP.append(ws)
     cfgs = [None, 0 | (1 << 8), 0 | (3 << 8), 3 | (1 << 8), 3 | (5 << 8)]
     if dtype == "bf16":     # the wide 8-wave tiles (ids after the halo configs): epilogue and split-K statistics
-        wide0 = L.jr_conv2d_num_configs(1) - WIDE_BF16
+        wide0 = WIDE0_BF16
         cfgs += [wide0 | (1 << 8), (wide0 + 1) | (1 << 8), (wide0 + 6) | (1 << 8), (wide0 + 2) | (3 << 8)]
     for cfg in cfgs + [-1]:
         if cfg is not None:

@@ -1,5 +1,6 @@
-"""Stream-K x8 convolutions (JR_F32_X8 ids 28..41: the stream-K grid of x8
-tile id - 28, k_conv SK in csrc/jr_conv.hip).
+"""Stream-K convolutions: JR_F32_X8 ids 28..41 (the stream-K grid of x8 tile
+id - 28, k_conv SK in csrc/jr_conv.hip) and JR_BF16 ids 33..57 (the stream-K
+grids of bf16 GEMM tiles 0..16 and wide tiles 0..7, k_conv_bf16 SK).
 
 A fixed grid of blocks walks equal ranges of the GEMM's tiles x K-tiles; a
 tile cut between blocks is finished by the block holding its first K-tile,
@@ -10,7 +11,9 @@ an agent-scope flag) in block order.  Checked here:
     test_gpu_ops.py (5e-6 / 1e-5 of max|ref|), on geometries whose tiles are
     cut into 2, 3 and 30+ pieces (the deep chains of a one-tile-row GEMM);
   * determinism: two runs are bitwise equal (fixed cut points, fixed order);
-  * grouped (ensemble members) stream-K: bitwise the per-member call.
+  * grouped (ensemble members) stream-K: bitwise the per-member call;
+  * bf16: fwd / dgrad / wgrad at the bf16 bars of test_gpu_bf16.py, with the
+    default and two forced grid sizes, reproducible run to run.
 Every other x8 id (and the stream-K ids on small shapes) is covered by
 test_gpu_ops.py::test_conv_every_tile_config.
 """
@@ -25,6 +28,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 X8, SK0 = 2, 28
+BF16, BF_SK0, BF_SKW0 = 1, 33, 50     # jr_conv.hip sk_base(JR_BF16): after the wide ids; wide tiles' at +17
 _KEEP = []
 
 
@@ -164,3 +168,26 @@ def test_stream_k_grouped_members():
             assert torch.equal(Yg[m * ym:(m + 1) * ym], Y) and torch.equal(Sg[m * 2 * cout:(m + 1) * 2 * cout], S)
     finally:
         ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, X8, 0, -1))
+
+
+@pytest.mark.parametrize("cfg", [BF_SK0 + 0, BF_SK0 + 3, BF_SK0 + 8, BF_SK0 + 11, BF_SK0 + 14, BF_SKW0 + 0,
+                                 BF_SKW0 + 1, BF_SKW0 + 6])
+@pytest.mark.parametrize("case", [c for c in CASES if c[3] % 8 == 0 or c[3] == 3])
+def test_stream_k_bf16(case, cfg):
+    import test_gpu_bf16 as B
+    ffi = _lib()
+    L = ffi.load()
+    assert L.jr_conv2d_num_configs(BF16) == BF_SKW0 + 8
+    n, h, w, cin, cout, kh, kw, s, pad = case
+    d, _, _ = B._desc(ffi, n, h, w, cin, cout, kh, kw, s, pad, (cin + 7) // 8 * 8)
+    try:
+        for grid in (0, 1, 3):       # planner grid, 128 and 384 blocks
+            outs = [B._run_all(ffi, L, case, seed=5, cfg=cfg | (grid << 8)) for _ in range(2)]
+            B._check(outs[0])
+            assert outs[0] == outs[1], (cfg, grid, outs)
+    finally:
+        for op in (0, 2):
+            ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), op, BF16, 0, -1))
+        if cin % 8 == 0:
+            for ph in range(s * s):
+                ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 1, BF16, ph, -1))
