@@ -49,8 +49,10 @@ def pinned_tile_table(conv_math: str, batch: int, height: int, width: int, train
     global _PINNED
     if _PINNED is None:
         # (JR_TILE_TABLES: another table file, for A/B runs of re-tuned tables)
-        p = os.environ.get("JR_TILE_TABLES") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                             "tiles_mi355x.json")
+        env = os.environ.get("JR_TILE_TABLES")
+        if env and not os.path.exists(env):
+            raise FileNotFoundError(f"JR_TILE_TABLES={env}: no such tile table file")
+        p = env or os.path.join(os.path.dirname(os.path.abspath(__file__)), "tiles_mi355x.json")
         _PINNED = json.load(open(p))["tables"] if os.path.exists(p) else []
     for t in _PINNED:
         if (t["conv_math"], t["batch"], t["height"], t["width"], t["train"]) == (conv_math, batch, height, width,
