@@ -2,11 +2,64 @@
 // capture (the error convention itself is host-only code: jr_error.cpp).
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
 #include <string>
+#include <tuple>
+#include <vector>
 
 #include "jr_common.h"
 
 namespace jr {
+
+namespace {
+struct Scratch {
+  unsigned* p = nullptr;
+  size_t words = 0;
+};
+std::mutex g_scratch_mu;
+std::map<std::tuple<int, hipStream_t, int>, Scratch> g_scratch;
+std::vector<unsigned*> g_scratch_kept;   // outgrown / captured regions: launches in flight may still use them
+
+unsigned* scratch_alloc(hipStream_t s, size_t words) {
+  void* p = nullptr;
+  if (hipMalloc(&p, words * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, words * sizeof(unsigned), s) != hipSuccess) return nullptr;
+  return static_cast<unsigned*>(p);
+}
+}  // namespace
+
+unsigned* stream_scratch(hipStream_t s, int kind, size_t words) {
+  words = std::max<size_t>(words, 1);
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+    // (the zeroing memset becomes a node of the graph ahead of the kernel;
+    // the kernel leaves the words zero, so every replay starts from zero;
+    // hipMalloc is not a stream operation: relaxed mode lets it through)
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    void* raw = nullptr;
+    const bool ok = hipMalloc(&raw, words * sizeof(unsigned)) == hipSuccess;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    unsigned* p = ok && hipMemsetAsync(raw, 0, words * sizeof(unsigned), s) == hipSuccess
+                      ? static_cast<unsigned*>(raw) : nullptr;
+    if (p) g_scratch_kept.push_back(p);
+    return p;
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  Scratch& e = g_scratch[std::make_tuple(dev, s, kind)];
+  if (e.words < words) {
+    const size_t n = std::max<size_t>(words, std::max<size_t>(2 * e.words, 16384));
+    unsigned* p = scratch_alloc(s, n);
+    if (!p) return nullptr;
+    if (e.p) g_scratch_kept.push_back(e.p);
+    e.p = p;
+    e.words = n;
+  }
+  return e.p;
+}
 
 int check_launch(const char* what) {
   const hipError_t e = hipGetLastError();

@@ -14,6 +14,14 @@ int check_launch(const char* what);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Device words the library owns per (device, stream, kind) (jr_api.cpp):
+// zeroed once when allocated (in order on that stream) and used only by
+// launches on that stream, which run in order -- so a kernel that leaves its
+// words zero again (the stream-K hand-off flags, kind 0) needs no memset
+// before each launch.  A capturing stream gets a fresh private region per
+// call: graph replays may run on any stream.  nullptr if allocation failed.
+unsigned* stream_scratch(hipStream_t s, int kind, size_t words);
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Bijective XCD-aware remap of a flat workgroup id (cdna_hip_programming.md

@@ -144,7 +144,9 @@ struct SplitFrag {
 // cut points are fixed by the grid, the sum order by the block order) before
 // its ordinary epilogue (store + fused BN statistics).  Waits point only to
 // higher blocks, which publish before waiting on anything, so no block waits
-// on one that cannot start; spins are bounded.
+// on one that cannot start; spins are bounded.  The flags are per-stream
+// library words (stream_scratch) that the consuming block resets, so a launch
+// needs no memset (one fill-kernel dispatch per stream-K GEMM before).
 template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0, bool SK = false>
 __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int WGN = 4 / WGM;
@@ -893,11 +895,10 @@ static int reduce_lanes(const Plan& p) {
   return G;
 }
 
-// stream-K: the hand-off flags (zeroed before each launch, a 16-B multiple
-// at the region's start), then one BM x BN fp32 partial slot per block
-static size_t sk_flag_bytes(const Plan& p) { return ((size_t)p.sk_blocks * 4 + 15) / 16 * 16; }
+// stream-K: one BM x BN fp32 partial slot per block (the hand-off flags are
+// stream_scratch words)
 static size_t plan_ws(const Plan& p) {
-  if (p.sk) return (sk_flag_bytes(p) + 255) / 256 * 256 + (size_t)p.sk_blocks * p.sk_slot * sizeof(float);
+  if (p.sk) return (size_t)p.sk_blocks * p.sk_slot * sizeof(float);
   return p.splits > 1 ? (size_t)p.splits * (size_t)p.M * (size_t)p.N * sizeof(float) : 0;
 }
 
@@ -1073,14 +1074,14 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     if (!ws || ws_bytes < plan_ws(p) + (members > 1 ? (size_t)(members - 1) * wsm : 0))
       return fail(JR_ERR_WORKSPACE, "conv: workspace too small for the stream-K hand-off");
     a.sk_ipb = p.sk_ipb;
-    a.sk_flags = static_cast<unsigned*>(ws);
-    a.sk_part = reinterpret_cast<float*>(static_cast<char*>(ws) + (sk_flag_bytes(p) + 255) / 256 * 256);
+    a.sk_part = static_cast<float*>(ws);
     a.sk_mb = (long long)wsm;
+    // the flags: zero at launch without a memset (every flag a block sets is
+    // reset by the one block that absorbs it)
+    a.sk_flags = stream_scratch(s, 0, (size_t)p.sk_blocks * members);
+    if (!a.sk_flags) return fail(JR_ERR_HIP, "conv: stream-K flag words could not be allocated");
+    a.sk_fmb = (long long)p.sk_blocks * sizeof(unsigned);
     grid = dim3(p.sk_blocks, members, 1);
-    // every polled word zeroed before EVERY launch (a memset node on the stream)
-    const hipError_t e = members > 1 ? hipMemset2DAsync(ws, wsm, 0, sk_flag_bytes(p), members, s)
-                                     : hipMemsetAsync(ws, 0, sk_flag_bytes(p), s);
-    if (e != hipSuccess) return fail(JR_ERR_HIP, "conv: stream-K flag reset failed");
   }
   if (is_halo(dtype, p.tile)) {
     const HaloCfg& h = kHaloBf16[p.tile - kNumCfgsBf16];

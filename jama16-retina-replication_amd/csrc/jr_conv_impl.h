@@ -47,9 +47,10 @@ struct ConvArgs {
   // the statistics partials and the final output (split-K reduce)
   long long a_mb, b_mb, c_mb, s_mb, o_mb;
   // stream-K (jr_conv.hip k_conv SK): iterations (tile-major, K-tile-minor)
-  // per block, the per-block hand-off flags (zeroed before every launch)
-  // and partial-tile slots; sk_mb = their member stride (grouped launches)
-  long long sk_ipb, sk_mb;
+  // per block, the per-block hand-off flags (stream_scratch words: zero at
+  // launch, and every flag set is reset by the block that consumes it) and
+  // the partial-tile slots (workspace); sk_fmb / sk_mb = their member strides
+  long long sk_ipb, sk_mb, sk_fmb;
   unsigned* sk_flags;
   float* sk_part;
 };
@@ -64,7 +65,7 @@ __device__ __forceinline__ void member_offsets(ConvArgs& g) {
     g.C = reinterpret_cast<float*>(reinterpret_cast<char*>(g.C) + m * g.c_mb);
     if (g.stats) g.stats = reinterpret_cast<float*>(reinterpret_cast<char*>(g.stats) + m * g.s_mb);
     if (g.sk_flags) {
-      g.sk_flags = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(g.sk_flags) + m * g.sk_mb);
+      g.sk_flags = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(g.sk_flags) + m * g.sk_fmb);
       g.sk_part = reinterpret_cast<float*>(reinterpret_cast<char*>(g.sk_part) + m * g.sk_mb);
     }
   }
@@ -203,6 +204,8 @@ __device__ __forceinline__ void sk_absorb(const ConvArgs& g, f32x16 (&acc)[TM][T
       if (__hip_atomic_load(g.sk_flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) break;
       __builtin_amdgcn_s_sleep(2);
     }
+    // the only reader of flag b: zero again for the stream's next launch
+    __hip_atomic_store(g.sk_flags + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below the poll)

@@ -191,3 +191,58 @@ def test_stream_k_bf16(case, cfg):
         if cin % 8 == 0:
             for ph in range(s * s):
                 ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 1, BF16, ph, -1))
+
+
+def test_stream_k_flags_reset_eager_and_graph():
+    """The hand-off flags are library words per stream that each launch
+    leaves zero (no memset per launch): back-to-back launches on one stream,
+    on a second stream, and replays of a captured graph (whose flag region is
+    private to the capture) all equal the first launch bitwise."""
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, cin, cout, kh, kw = 4, 8, 8, 2048, 384, 1, 1     # 30+ pieces per tile
+    d = ffi.ConvDesc(n, h, w, cin, cout, kh, kw, 1, 1, 0, 0, h, w, 0, cin, 0, cout)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    X = torch.randn(n * h * w * cin, device="cuda", generator=g)
+    W = torch.randn(kh * kw * cin * cout, device="cuda", generator=g) * 0.02
+    ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, X8, 0, SK0 + 11))
+    try:
+        wsb = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, X8)
+        ws = torch.zeros(wsb // 4 + 4, device="cuda")
+
+        def fwd(Y, stream=None):
+            ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), X8, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
+                                             ws.data_ptr(), wsb, stream))
+        ref = torch.zeros(n * h * w * cout, device="cuda")
+        fwd(ref)
+        torch.cuda.synchronize()
+        for _ in range(5):
+            Y = torch.zeros_like(ref)
+            fwd(Y)
+            torch.cuda.synchronize()
+            assert torch.equal(Y, ref)
+        side = torch.cuda.Stream()
+        for _ in range(3):
+            Y = torch.zeros_like(ref)
+            fwd(Y, ctypes.c_void_p(side.cuda_stream))
+            side.synchronize()
+            assert torch.equal(Y, ref)
+        cap = torch.cuda.Stream()
+        Yg = torch.zeros_like(ref)
+        sp = ctypes.c_void_p(cap.cuda_stream)
+        ffi.check("begin", L.jr_graph_begin(sp))
+        fwd(Yg, sp)
+        ex = ctypes.c_void_p()
+        ffi.check("end", L.jr_graph_end(sp, ctypes.byref(ex)))
+        try:
+            for _ in range(4):
+                Yg.zero_()
+                torch.cuda.synchronize()
+                ffi.check("launch", L.jr_graph_launch(ex, sp))
+                cap.synchronize()
+                assert torch.equal(Yg, ref)
+        finally:
+            ffi.check("destroy", L.jr_graph_destroy(ex))
+        assert float(ref.abs().max()) > 0
+    finally:
+        ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, X8, 0, -1))
