@@ -38,6 +38,7 @@
 #include "jr_conv_impl.h"
 
 #include <array>
+#include <cstdlib>
 #include <type_traits>
 #include <map>
 #include <mutex>
@@ -803,7 +804,19 @@ static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
 constexpr int kSkBlocks = 512;     // stream-K grid: 2 x 256 CUs
 constexpr int kSkMinIters = 4;     // K-tiles per stream-K block at least
 
-static Plan plan_with(int dtype, int cfg, int M, int N, int K) {
+// Blocks the planner's split-K factor aims for (>= 2.5 per CU); filter
+// gradients may aim lower (JR_WGRAD_SPLIT_TARGET, an A/B knob read once):
+// their slabs are summed by the deferred k_wgrad_reduce from HBM.
+static int split_target(int op) {
+  static const int wg = [] {
+    const char* e = std::getenv("JR_WGRAD_SPLIT_TARGET");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 640;
+  }();
+  return op == OP_WGRAD ? wg : 640;
+}
+
+static Plan plan_with(int dtype, int cfg, int M, int N, int K, int op) {
   Plan p{};
   p.M = M; p.N = N; p.K = K; p.cfg = cfg; p.tile = cfg_tile(cfg);
   const TileCfg& t = tile_cfg(dtype, p.tile);
@@ -812,7 +825,7 @@ static Plan plan_with(int dtype, int cfg, int M, int N, int K) {
   p.ktiles = (int)ceil_div(K, t.bk);
   const int tiles = p.mt * p.nt;
   int splits = 1;
-  const int target = 640;   // >= 2.5 blocks per CU
+  const int target = split_target(op);
   if (tiles < target) {
     splits = (int)ceil_div(target, tiles);
     const int max_by_k = std::max(1, p.ktiles / 8);
@@ -883,7 +896,7 @@ static Plan make_plan(int dtype, int op, int M, int N, int K, const jr_conv_desc
   // a halo config (tuned, pinned or forced) only where its geometry holds
   if (cfg < 0 || (is_halo(dtype, cfg_tile(cfg)) && !halo_ok(d, op, dtype, cfg_tile(cfg))))
     cfg = heuristic_cfg(dtype, M, N, K);
-  return plan_with(dtype, cfg, M, N, K);
+  return plan_with(dtype, cfg, M, N, K, op);
 }
 
 // z-lanes per float4 column of the split-K reduce (k_splitk_reduce and the
@@ -1210,7 +1223,7 @@ static Plan dgrad_phase_plan(const jr_conv_desc* d, int dtype, const Phase& p, i
   *ok = p.hc > 0 && p.wc > 0;
   if (p.na == 0 || p.nb == 0) {
     const int M = d->n * p.hc * p.wc;
-    Plan pl = plan_with(dtype, heuristic_cfg(dtype, M, d->c_in, 16), M, d->c_in, 16);
+    Plan pl = plan_with(dtype, heuristic_cfg(dtype, M, d->c_in, 16), M, d->c_in, 16, OP_DGRAD);
     pl.K = 0; pl.ktiles = 0; pl.splits = 1; pl.kt_per_split = 1;
     return pl;
   }
@@ -1292,7 +1305,7 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
     float best_t = 1e30f;
     auto time_cfg = [&](int c) -> float {
       if (is_halo(dtype, cfg_tile(c)) && !halo_ok(d, op, dtype, cfg_tile(c))) return 1e30f;
-      const Plan pc = plan_with(dtype, c, M, N, K);
+      const Plan pc = plan_with(dtype, c, M, N, K, op);
       // FWD runs with the fused BN statistics: their partials must fit too
       if ((op == OP_FWD ? align256(plan_ws(pc)) + stats_ws(dtype, pc) : plan_ws(pc)) > ws_bytes) return 1e30f;
       rc = run_conv(d, op, dtype, A, B, C, 0, ws, ws_bytes, stream, c, op == OP_DGRAD ? i : -1);  // warm-up
@@ -1309,8 +1322,8 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
       // written and re-read through HBM, which a back-to-back timing on a hot
       // L2 undercounts): more splits must win by 2 %, fewer may lose by 2 %
       const int ps = pc.splits > 1 ? pc.splits : 0;
-      const int bs = best_t < 1e29f ? (plan_with(dtype, best_c, M, N, K).splits > 1
-                                           ? plan_with(dtype, best_c, M, N, K).splits : 0) : 0;
+      const int bs = best_t < 1e29f ? (plan_with(dtype, best_c, M, N, K, op).splits > 1
+                                           ? plan_with(dtype, best_c, M, N, K, op).splits : 0) : 0;
       const float bar = ps > bs ? 0.98f : ps < bs ? 1.02f : 1.0f;
       if (ms < best_t * bar) { best_t = ms; best_c = c; }
       return ms;
@@ -1325,7 +1338,7 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
         if (tile_t[k] < 1e29f && (c < 0 || tile_t[k] < tile_t[c])) c = k;
       if (c < 0) break;
       tile_t[c] = 1e30f;
-      const Plan dp = plan_with(dtype, c, M, N, K);
+      const Plan dp = plan_with(dtype, c, M, N, K, op);
       if (dp.sk) {   // stream-K: other grid sizes (128 x v blocks) instead of split factors
         for (int v : {2, 3, 6, 8}) {
           time_cfg(c | (v << kSplitShift));
