@@ -235,6 +235,14 @@ int jr_maxpool3x3s2_fwd(const jr_pool_desc* d, int dtype, const void* x, void* y
                         void* stream);
 int jr_maxpool3x3s2_bwd(const jr_pool_desc* d, int dtype, const uint8_t* argmax, const void* dy,
                         void* dx, int accumulate, void* stream);
+/* The fused forward of a conv2d_bn layer whose only reader is a max-pool
+ * (the stem's conv2d_3 / conv2d_5 outputs): raw is the conv output (the
+ * descriptor's x slice), each tap is max(bn_pre(raw), 0) in the path dtype
+ * (jr_bn_relu_apply's value), then the max-pool as jr_maxpool3x3s2_fwd --
+ * y and argmax bitwise the two calls', without the full-resolution
+ * activation.  mean / invstd / beta: [c] fp32. */
+int jr_bn_relu_maxpool3x3s2_fwd(const jr_pool_desc* d, int dtype, const void* raw, const float* mean,
+                                const float* invstd, const float* beta, void* y, uint8_t* argmax, void* stream);
 int jr_avgpool3x3s1_fwd(const jr_pool_desc* d, int dtype, const void* x, void* y, void* stream);
 int jr_avgpool3x3s1_bwd(const jr_pool_desc* d, int dtype, const void* dy, void* dx, int accumulate,
                         void* stream);

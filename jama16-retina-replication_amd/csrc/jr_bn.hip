@@ -44,13 +44,7 @@ constexpr int kAppUnroll = JR_BN_APP_UNROLL;  // rows per thread in the elementw
 // load into the conditional block of its only use (one wait per row).
 __device__ __forceinline__ void pin(uint4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
 
-// Same rounding in fwd and bwd so the ReLU mask is bit-identical.
-__device__ __forceinline__ float bn_xhat(float x, float mean, float invstd) {
-  return __fmul_rn(__fsub_rn(x, mean), invstd);
-}
-__device__ __forceinline__ float bn_pre(float x, float mean, float invstd, float beta) {
-  return __fadd_rn(bn_xhat(x, mean, invstd), beta);
-}
+// (bn_xhat / bn_pre: jr_common.h, shared with the fused BN + max-pool)
 
 // One 16-byte vector of channels: 4 fp32 or 8 bf16, widened to fp32.
 template <typename T> struct Vec;

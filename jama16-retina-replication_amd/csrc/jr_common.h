@@ -43,6 +43,16 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return *reinterpret_cast<uint16_t*>(&h);
 }
 
+// BatchNormalization(scale=False) pre-activation, in one fixed rounding
+// order: every kernel that applies or differentiates it (jr_bn.hip, the
+// fused BN + max-pool of jr_pool.hip) sees bit-identical values and ReLU masks.
+__device__ __forceinline__ float bn_xhat(float x, float mean, float invstd) {
+  return __fmul_rn(__fsub_rn(x, mean), invstd);
+}
+__device__ __forceinline__ float bn_pre(float x, float mean, float invstd, float beta) {
+  return __fadd_rn(bn_xhat(x, mean, invstd), beta);
+}
+
 // Element load/store of an activation in the path dtype.
 template <typename T> struct Elt;
 template <> struct Elt<float> {

@@ -72,6 +72,59 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(jr_pool_desc d, const T* __
   }
 }
 
+// BN + ReLU + max-pool in one pass (the stem's conv2d_3 / conv2d_5 outputs,
+// whose only reader is the max-pool): every window tap is the raw conv output
+// put through bn_pre and ReLU -- and rounded to the path dtype, exactly as
+// k_bn_relu_apply stores it -- before the comparison, so y and argmax are
+// bitwise the two-kernel result, without writing and re-reading the
+// full-resolution activation (354 / 248 MB per fp32 step).
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_relu_maxpool_fwd(jr_pool_desc d, const T* __restrict__ x,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd,
+                                                             const float* __restrict__ beta, T* y, uint8_t* argmax) {
+  const int c4 = d.c >> 2;
+  const int total = d.n * d.ho * d.wo * c4;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int q = e % c4;
+    const int pix = e / c4;
+    const int ow = pix % d.wo;
+    const int t = pix / d.wo;
+    const int oh = t % d.ho;
+    const int b = t / d.ho;
+    float mu[4], is[4], be[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mu[j] = mean[q * 4 + j];
+      is[j] = invstd[q * 4 + j];
+      be[j] = beta[q * 4 + j];
+    }
+    float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int arg[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int ih = oh * 2 + r, iw = ow * 2 + c;
+        const float4 v = P4<T>::ld(x + ((int64_t)(b * d.h + ih) * d.w + iw) * d.x_c_stride + d.x_c_off + q * 4);
+        const float va[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float a = fmaxf(bn_pre(va[j], mu[j], is[j], be[j]), 0.f);
+          if constexpr (sizeof(T) == 2) a = bf2f(f2bf(a));
+          if (a > best[j] || (r == 0 && c == 0)) { best[j] = a; arg[j] = r * 3 + c; }
+        }
+      }
+    }
+    P4<T>::st(y + (int64_t)pix * d.y_c_stride + d.y_c_off + q * 4, make_float4(best[0], best[1], best[2], best[3]));
+    if (argmax) {
+      const uint32_t packed = (uint32_t)arg[0] | ((uint32_t)arg[1] << 8) | ((uint32_t)arg[2] << 16) |
+                              ((uint32_t)arg[3] << 24);
+      *reinterpret_cast<uint32_t*>(argmax + (int64_t)pix * d.c + q * 4) = packed;
+    }
+  }
+}
+
 // Backward as a gather over 2x2 input cells: input rows 2a, 2a+1 and columns
 // 2b, 2b+1 are covered only by the windows oh in {a-1, a}, ow in {b-1, b}, so
 // one thread loads those (at most) four windows' dy and argmax once and writes
@@ -300,6 +353,22 @@ JR_API int jr_maxpool3x3s2_fwd(const jr_pool_desc* d, int dtype, const void* x, 
     hipLaunchKernelGGL(k_maxpool_fwd<uint16_t>, dim3(g), dim3(256), 0, as_stream(stream), *d,
                        (const uint16_t*)x, (uint16_t*)y, argmax);
   return check_launch("maxpool_fwd");
+}
+
+JR_API int jr_bn_relu_maxpool3x3s2_fwd(const jr_pool_desc* d, int dtype, const void* raw, const float* mean,
+                                       const float* invstd, const float* beta, void* y, uint8_t* argmax,
+                                       void* stream) {
+  int rc = check_pool(d, dtype, true);
+  if (rc) return rc;
+  if (!raw || !mean || !invstd || !beta || !y) return fail(JR_ERR_INVALID, "bn_relu_maxpool_fwd: null pointer");
+  const int g = grid_for((int64_t)d->n * d->ho * d->wo * (d->c / 4));
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_bn_relu_maxpool_fwd<float>, dim3(g), dim3(256), 0, as_stream(stream), *d,
+                       (const float*)raw, mean, invstd, beta, (float*)y, argmax);
+  else
+    hipLaunchKernelGGL(k_bn_relu_maxpool_fwd<uint16_t>, dim3(g), dim3(256), 0, as_stream(stream), *d,
+                       (const uint16_t*)raw, mean, invstd, beta, (uint16_t*)y, argmax);
+  return check_launch("bn_relu_maxpool_fwd");
 }
 
 JR_API int jr_maxpool3x3s2_bwd(const jr_pool_desc* d, int dtype, const uint8_t* argmax, const void* dy,

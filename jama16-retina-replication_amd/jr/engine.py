@@ -69,7 +69,7 @@ class Engine:
                  optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
                  head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None,
                  autotune: bool = False, tiles: str = "pinned", fuse_siblings: bool = True, lanes: int = 2,
-                 conv_math: Optional[str] = None, defer_wgrad: bool = True):
+                 conv_math: Optional[str] = None, defer_wgrad: bool = True, fuse_pool: Optional[bool] = None):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if conv_math is None:            # fp32 default: x8 (fp32-accurate, on the bf16 matrix cores)
@@ -120,6 +120,12 @@ class Engine:
         self._join_ev = [torch.cuda.Event() for _ in range(self.nlanes - 1)]
         self._tail_ev = [torch.cuda.Event() for _ in range(self.nlanes)]
         self.plan = build_plan(self.g, fuse_siblings)
+        # conv2d_bn outputs read only by a max-pool (the stem's conv2d_3 and
+        # conv2d_5): BN + ReLU run inside the pool (jr_bn_relu_maxpool3x3s2_fwd)
+        # and the full-resolution activation is never written
+        if fuse_pool is None:           # (JR_FUSE_POOL=0: the separate apply + max-pool, for A/B runs)
+            fuse_pool = os.environ.get("JR_FUSE_POOL", "1") != "0"
+        self.pool_fused = self._fusable_pools() if fuse_pool else {}
         self.cunits: List[ConvUnit] = self.plan.units
         self.layout, self.nparam = self.plan.layout, self.plan.nparam
         self._alloc()
@@ -157,6 +163,23 @@ class Engine:
     # ------------------------------------------------------------------ memory
     def _t(self, n: int, dtype=torch.float32) -> torch.Tensor:
         return torch.zeros(int(n), dtype=dtype, device=self.device)
+
+    def _fusable_pools(self) -> Dict[int, int]:
+        """max-pool node index -> its input buffer, for every max-pool whose
+        input is the whole output of ONE single-member conv launch and read
+        by nothing else."""
+        g, out = self.g, {}
+        for i, n in enumerate(g.nodes):
+            if n.kind != "maxpool":
+                continue
+            prod = [m for m in g.nodes if m.y.buf == n.x]
+            readers = [m for m in g.nodes if m.x == n.x]
+            if len(prod) != 1 or len(readers) != 1 or prod[0].kind != "conv":
+                continue
+            u = self.plan.unit_of[prod[0].idx]
+            if len(u.members) == 1 and prod[0].y.c_off == 0 and prod[0].cout == g.bufs[n.x].c:
+                out[i] = n.x
+        return out
 
     def _alloc(self) -> None:
         g, B = self.g, self.batch
@@ -522,6 +545,7 @@ class Engine:
         AX = (lambda bid: self.aplanes[bid].data_ptr()) if x8p else A  # noqa: E731
         ax_reads = (lambda bid: [("ap", bid)]) if x8p else a_all  # noqa: E731
         split_done = set()
+        fused_bufs = set(self.pool_fused.values())
         for i, n in enumerate(g.nodes):
             ln = lane_of[i]
             s, ws = S[ln], WS[ln]
@@ -549,6 +573,8 @@ class Engine:
                                                     self.invstd_unit[uid].data_ptr(), ws, wsb, s),
                     "conv_fwd", ln, ax_reads(u.x) + [wkey], [("r", uid), ("ws", ln)])
                 for m, co in zip(u.members, u.col_off):
+                    if m.y.buf in fused_bufs:
+                        continue        # applied inside its max-pool
                     yb = g.bufs[m.y.buf]
                     add(fwd, L.jr_bn_relu_apply, (dt, raw, co, u.cout, M, m.cout, self.mean[m.idx].data_ptr(),
                                                   self.invstd[m.idx].data_ptr(),
@@ -556,6 +582,18 @@ class Engine:
                                                   A(m.y.buf), m.y.c_off, yb.c, s),
                         "bn_relu", ln, [("r", uid), ("p",)], [("a", m.y.buf, m.y.c_off)],
                         nbytes=2 * M * m.cout * self.esz)
+            elif n.kind == "maxpool" and i in self.pool_fused:
+                d = self._pool_desc(n, B)
+                pn = next(m for m in g.nodes if m.y.buf == n.x)          # the conv2d_bn layer it applies
+                d.x_c_off, d.x_c_stride = 0, pn.cout                       # its raw output
+                keep.append(d)
+                puid = unit_of[pn.idx].first.idx
+                add(fwd, L.jr_bn_relu_maxpool3x3s2_fwd, (ctypes.byref(d), dt, self.raw_unit[puid].data_ptr(),
+                                                         self.mean[pn.idx].data_ptr(), self.invstd[pn.idx].data_ptr(),
+                                                         self._p(f"batch_normalization_{pn.idx + 1}/beta"),
+                                                         A(n.y.buf), self.argmax[i].data_ptr(), s),
+                    "bn_relu_maxpool_fwd", ln, [("r", puid), ("p",)], [("a", n.y.buf, n.y.c_off), ("am", i)],
+                    nbytes=B * n.c * (n.h * n.w * self.esz + n.ho * n.wo * (self.esz + 1)))
             elif n.kind == "maxpool":
                 d = self._pool_desc(n, B)
                 keep.append(d)

@@ -165,6 +165,37 @@ def test_sibling_fusion_matches_unfused(dtype):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_fused_bn_maxpool_is_bitwise(dtype):
+    """The stem's conv2d_3 / conv2d_5 BN + ReLU applied inside their max-pools
+    (jr_bn_relu_maxpool3x3s2_fwd, the full-resolution activation never
+    written): pooled outputs, argmax and the weights after three steps are
+    bitwise those of the separate apply + max-pool, at 299^2."""
+    from jr.engine import Engine
+    from jr import synth
+    imgs = synth.fundus_batch(5, 2, 299)
+    y = np.array([[1.0], [0.0]], np.float32)
+    e = {f: Engine(2, 299, 299, seed=4, dtype=dtype, fuse_pool=f) for f in (True, False)}
+    assert sorted(e[True].pool_fused) == [i for i, n in enumerate(e[True].g.nodes) if n.kind == "maxpool"][:2]
+    assert not e[False].pool_fused
+    for k in e.values():
+        k.set_batch(imgs, y)
+        k.forward()
+    for k in e.values():
+        k.synchronize()
+    for i, b in e[True].pool_fused.items():
+        n = e[True].g.nodes[i]
+        assert torch.equal(e[True].argmax[i], e[False].argmax[i])
+        assert torch.equal(e[True].acts[n.y.buf], e[False].acts[n.y.buf])
+        assert float(e[False].acts[b].float().abs().max()) > 0
+    for _ in range(3):
+        for k in e.values():
+            k.train_step()
+    for k in e.values():
+        k.synchronize()
+    assert np.array_equal(e[True].params_numpy(), e[False].params_numpy())
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_lanes_are_bitwise_single_stream(dtype):
     """Branch-level concurrency (jr.lanes): the engine's own call schedule
     orders every conflicting pair across lanes, and 4 lanes (eager) and 2

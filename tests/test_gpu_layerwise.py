@@ -59,8 +59,10 @@ def test_every_layer_teacher_forced(dtype, res, batch):
     from jr import synth
 
     tol = TOL["f32" if dtype == "f32x8" else dtype]      # x8 is held to the fp32 tolerances
+    # (fuse_pool=False: every activation buffer materialised for the per-layer
+    # checks; the fused BN + max-pool is bitwise the pair, test_gpu_engine.py)
     eng = Engine(batch, res, res, seed=7, dtype="f32" if dtype == "f32x8" else dtype,
-                 conv_math={"f32": "f32", "f32x8": "x8"}.get(dtype))
+                 conv_math={"f32": "f32", "f32x8": "x8"}.get(dtype), fuse_pool=False)
     imgs = synth.fundus_batch(3, batch, res)
     y = np.array([[1.0], [0.0], [1.0], [0.0]][:batch], np.float32)
     eng.set_batch(imgs, y)

@@ -11,7 +11,7 @@ from oracle.inception_ref import InceptionV3Ref
 res = int(sys.argv[1]) if len(sys.argv) > 1 else 107
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 dtype = sys.argv[3] if len(sys.argv) > 3 else "f32"
-eng = Engine(B, res, res, seed=1, dtype=dtype)
+eng = Engine(B, res, res, seed=1, dtype=dtype, fuse_pool=False)   # every activation materialised
 imgs = synth.fundus_batch(0, B, res)
 y = synth.labels(0, B)
 eng.set_batch(imgs, y)
