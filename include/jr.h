@@ -243,6 +243,13 @@ int jr_maxpool3x3s2_bwd(const jr_pool_desc* d, int dtype, const uint8_t* argmax,
  * activation.  mean / invstd / beta: [c] fp32. */
 int jr_bn_relu_maxpool3x3s2_fwd(const jr_pool_desc* d, int dtype, const void* raw, const float* mean,
                                 const float* invstd, const float* beta, void* y, uint8_t* argmax, void* stream);
+/* The same over the members of an ensemble as one batch of d->n images:
+ * image b belongs to member b / images_per_member, whose mean / invstd sit
+ * stats_member_stride and beta beta_member_stride floats further. */
+int jr_bn_relu_maxpool3x3s2_fwd_grouped(const jr_pool_desc* d, int dtype, int32_t images_per_member,
+                                        const void* raw, const float* mean, const float* invstd,
+                                        int64_t stats_member_stride, const float* beta, int64_t beta_member_stride,
+                                        void* y, uint8_t* argmax, void* stream);
 int jr_avgpool3x3s1_fwd(const jr_pool_desc* d, int dtype, const void* x, void* y, void* stream);
 int jr_avgpool3x3s1_bwd(const jr_pool_desc* d, int dtype, const void* dy, void* dx, int accumulate,
                         void* stream);

@@ -77,12 +77,15 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(jr_pool_desc d, const T* __
 // put through bn_pre and ReLU -- and rounded to the path dtype, exactly as
 // k_bn_relu_apply stores it -- before the comparison, so y and argmax are
 // bitwise the two-kernel result, without writing and re-reading the
-// full-resolution activation (354 / 248 MB per fp32 step).
+// full-resolution activation (354 / 248 MB per fp32 step).  Grouped
+// (ensemble members): image b belongs to member b / ipm, whose statistics
+// and beta sit st_mb / be_mb floats further (0 for one member).
 template <typename T>
 __global__ void __launch_bounds__(256) k_bn_relu_maxpool_fwd(jr_pool_desc d, const T* __restrict__ x,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ invstd,
-                                                             const float* __restrict__ beta, T* y, uint8_t* argmax) {
+                                                             const float* __restrict__ beta, T* y, uint8_t* argmax,
+                                                             int ipm, long long st_mb, long long be_mb) {
   const int c4 = d.c >> 2;
   const int total = d.n * d.ho * d.wo * c4;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
@@ -92,12 +95,13 @@ __global__ void __launch_bounds__(256) k_bn_relu_maxpool_fwd(jr_pool_desc d, con
     const int t = pix / d.wo;
     const int oh = t % d.ho;
     const int b = t / d.ho;
+    const long long mem = b / ipm;
     float mu[4], is[4], be[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      mu[j] = mean[q * 4 + j];
-      is[j] = invstd[q * 4 + j];
-      be[j] = beta[q * 4 + j];
+      mu[j] = mean[mem * st_mb + q * 4 + j];
+      is[j] = invstd[mem * st_mb + q * 4 + j];
+      be[j] = beta[mem * be_mb + q * 4 + j];
     }
     float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     int arg[4] = {0, 0, 0, 0};
@@ -355,20 +359,33 @@ JR_API int jr_maxpool3x3s2_fwd(const jr_pool_desc* d, int dtype, const void* x, 
   return check_launch("maxpool_fwd");
 }
 
-JR_API int jr_bn_relu_maxpool3x3s2_fwd(const jr_pool_desc* d, int dtype, const void* raw, const float* mean,
-                                       const float* invstd, const float* beta, void* y, uint8_t* argmax,
-                                       void* stream) {
+JR_API int jr_bn_relu_maxpool3x3s2_fwd_grouped(const jr_pool_desc* d, int dtype, int32_t images_per_member,
+                                               const void* raw, const float* mean, const float* invstd,
+                                               int64_t stats_member_stride, const float* beta,
+                                               int64_t beta_member_stride, void* y, uint8_t* argmax, void* stream) {
   int rc = check_pool(d, dtype, true);
   if (rc) return rc;
   if (!raw || !mean || !invstd || !beta || !y) return fail(JR_ERR_INVALID, "bn_relu_maxpool_fwd: null pointer");
+  if (images_per_member < 1 || stats_member_stride < 0 || beta_member_stride < 0)
+    return fail(JR_ERR_INVALID, "bn_relu_maxpool_fwd: bad member geometry");
   const int g = grid_for((int64_t)d->n * d->ho * d->wo * (d->c / 4));
   if (dtype == JR_F32)
     hipLaunchKernelGGL(k_bn_relu_maxpool_fwd<float>, dim3(g), dim3(256), 0, as_stream(stream), *d,
-                       (const float*)raw, mean, invstd, beta, (float*)y, argmax);
+                       (const float*)raw, mean, invstd, beta, (float*)y, argmax, images_per_member,
+                       (long long)stats_member_stride, (long long)beta_member_stride);
   else
     hipLaunchKernelGGL(k_bn_relu_maxpool_fwd<uint16_t>, dim3(g), dim3(256), 0, as_stream(stream), *d,
-                       (const uint16_t*)raw, mean, invstd, beta, (uint16_t*)y, argmax);
+                       (const uint16_t*)raw, mean, invstd, beta, (uint16_t*)y, argmax, images_per_member,
+                       (long long)stats_member_stride, (long long)beta_member_stride);
   return check_launch("bn_relu_maxpool_fwd");
+}
+
+JR_API int jr_bn_relu_maxpool3x3s2_fwd(const jr_pool_desc* d, int dtype, const void* raw, const float* mean,
+                                       const float* invstd, const float* beta, void* y, uint8_t* argmax,
+                                       void* stream) {
+  if (!d) return fail(JR_ERR_INVALID, "pool: null descriptor");
+  return jr_bn_relu_maxpool3x3s2_fwd_grouped(d, dtype, d->n > 0 ? d->n : 1, raw, mean, invstd, 0, beta, 0, y,
+                                             argmax, stream);
 }
 
 JR_API int jr_maxpool3x3s2_bwd(const jr_pool_desc* d, int dtype, const uint8_t* argmax, const void* dy,

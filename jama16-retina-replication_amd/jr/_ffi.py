@@ -124,6 +124,8 @@ _SIGS = {
                                     c_void_p]),
     "jr_bn_relu_maxpool3x3s2_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_void_p]),
+    "jr_bn_relu_maxpool3x3s2_fwd_grouped": (c_int, [POINTER(PoolDesc), c_int, c_int32, c_void_p, c_void_p, c_void_p,
+                                                    c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "jr_maxpool3x3s2_bwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p]),
     "jr_avgpool3x3s1_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p]),

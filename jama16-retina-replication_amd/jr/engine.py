@@ -44,6 +44,25 @@ DTYPES = {"f32": _ffi.JR_F32, "bf16": _ffi.JR_BF16}
 _PINNED = None
 
 
+def fusable_pools(g: Graph, plan) -> Dict[int, int]:
+    """max-pool node index -> its input buffer, for every max-pool whose
+    input is the whole output of ONE single-member conv launch and read by
+    nothing else (the stem's conv2d_3 and conv2d_5): BN + ReLU then run
+    inside the pool (jr_bn_relu_maxpool3x3s2_fwd)."""
+    out = {}
+    for i, n in enumerate(g.nodes):
+        if n.kind != "maxpool":
+            continue
+        prod = [m for m in g.nodes if m.y.buf == n.x]
+        readers = [m for m in g.nodes if m.x == n.x]
+        if len(prod) != 1 or len(readers) != 1 or prod[0].kind != "conv":
+            continue
+        u = plan.unit_of[prod[0].idx]
+        if len(u.members) == 1 and prod[0].y.c_off == 0 and prod[0].cout == g.bufs[n.x].c:
+            out[i] = n.x
+    return out
+
+
 def pinned_tile_table(conv_math: str, batch: int, height: int, width: int, train: bool) -> Optional[dict]:
     """The committed tile table (jr/tiles_mi355x.json) of this workload, or None."""
     global _PINNED
@@ -125,7 +144,7 @@ class Engine:
         # and the full-resolution activation is never written
         if fuse_pool is None:           # (JR_FUSE_POOL=0: the separate apply + max-pool, for A/B runs)
             fuse_pool = os.environ.get("JR_FUSE_POOL", "1") != "0"
-        self.pool_fused = self._fusable_pools() if fuse_pool else {}
+        self.pool_fused = fusable_pools(self.g, self.plan) if fuse_pool else {}
         self.cunits: List[ConvUnit] = self.plan.units
         self.layout, self.nparam = self.plan.layout, self.plan.nparam
         self._alloc()
@@ -163,23 +182,6 @@ class Engine:
     # ------------------------------------------------------------------ memory
     def _t(self, n: int, dtype=torch.float32) -> torch.Tensor:
         return torch.zeros(int(n), dtype=dtype, device=self.device)
-
-    def _fusable_pools(self) -> Dict[int, int]:
-        """max-pool node index -> its input buffer, for every max-pool whose
-        input is the whole output of ONE single-member conv launch and read
-        by nothing else."""
-        g, out = self.g, {}
-        for i, n in enumerate(g.nodes):
-            if n.kind != "maxpool":
-                continue
-            prod = [m for m in g.nodes if m.y.buf == n.x]
-            readers = [m for m in g.nodes if m.x == n.x]
-            if len(prod) != 1 or len(readers) != 1 or prod[0].kind != "conv":
-                continue
-            u = self.plan.unit_of[prod[0].idx]
-            if len(u.members) == 1 and prod[0].y.c_off == 0 and prod[0].cout == g.bufs[n.x].c:
-                out[i] = n.x
-        return out
 
     def _alloc(self) -> None:
         g, B = self.g, self.batch

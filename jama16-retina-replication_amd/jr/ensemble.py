@@ -23,13 +23,14 @@ that member (tests/test_gpu_ensemble.py).  Inference only (train=False).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional
 
 import numpy as np
 import torch
 
 from . import _ffi
-from .engine import DTYPES, pinned_tile_table
+from .engine import DTYPES, fusable_pools, pinned_tile_table
 from .inception import BN_EPS, build_inception_v3
 from .plan import build_plan
 
@@ -39,7 +40,7 @@ class EnsembleEngine:
 
     def __init__(self, params: List[np.ndarray], batch: int, height: int = 299, width: int = 299, units: int = 1,
                  device: int | torch.device = 0, dtype: str = "f32", conv_math: Optional[str] = None,
-                 tiles: str = "pinned", head: str = "sigmoid"):
+                 tiles: str = "pinned", head: str = "sigmoid", fuse_pool: Optional[bool] = None):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if conv_math is None:
@@ -56,6 +57,10 @@ class EnsembleEngine:
         self.g = build_inception_v3(height, width, units)
         self.units = self.g.units
         self.plan = build_plan(self.g, True)
+        if fuse_pool is None:            # (as jr.Engine: JR_FUSE_POOL=0 keeps the separate apply + max-pool)
+            fuse_pool = os.environ.get("JR_FUSE_POOL", "1") != "0"
+        # the stem's BN + ReLU inside its max-pools, every member in one launch
+        self.pool_fused = fusable_pools(self.g, self.plan) if fuse_pool else {}
         self.cunits = self.plan.units
         self.nparam = self.plan.nparam
         self.members = len(params)
@@ -181,7 +186,8 @@ class EnsembleEngine:
         calls, keep = [], []
         A = lambda bid: self.acts[bid].data_ptr()  # noqa: E731
         ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
-        for n in g.nodes:
+        fused_bufs = set(self.pool_fused.values())
+        for i, n in enumerate(g.nodes):
             if n.kind == "conv":
                 u = self.plan.unit_of[n.idx]
                 if u.first is not n:
@@ -202,6 +208,8 @@ class EnsembleEngine:
                                self.raw_ms[uid], BN_EPS, mean, inv, self.stats_ms, ws, wsb, s), "conv_fwd"))
                 rows = B * u.ho * u.wo
                 for mem, co in zip(u.members, u.col_off):
+                    if mem.y.buf in fused_bufs:
+                        continue        # applied inside its max-pool
                     yb = g.bufs[mem.y.buf]
                     calls.append((L.jr_bn_relu_apply_grouped,
                                   (self.dt, M, raw, co, u.cout, self.raw_ms[uid], rows, mem.cout, mean + 4 * co,
@@ -219,7 +227,17 @@ class EnsembleEngine:
                     keep.append(d)
                     xi = A(n.x) + self.esz * m * self.act_ms[n.x]
                     yo = A(n.y.buf) + self.esz * m * self.act_ms[n.y.buf]
-                    if n.kind == "maxpool":
+                    if i in self.pool_fused:    # BN + ReLU of the producing layer on the fly
+                        pn = next(q for q in g.nodes if q.y.buf == n.x)
+                        puid = self.plan.unit_of[pn.idx].first.idx
+                        so = self.stat_off[puid]
+                        mean = self.stats.data_ptr() + 4 * (so + m * self.stats_ms)
+                        calls.append((L.jr_bn_relu_maxpool3x3s2_fwd_grouped,
+                                      (ctypes.byref(d), self.dt, B, self.raw_unit[puid].data_ptr()
+                                       + self.esz * m * self.raw_ms[puid], mean, mean + 4 * pn.cout, self.stats_ms,
+                                       self._p(m, f"batch_normalization_{pn.idx + 1}/beta"), self.nparam, yo, None, s),
+                                      "bn_relu_maxpool_fwd"))
+                    elif n.kind == "maxpool":
                         calls.append((L.jr_maxpool3x3s2_fwd, (ctypes.byref(d), self.dt, xi, yo, None, s),
                                       "maxpool_fwd"))
                     else:

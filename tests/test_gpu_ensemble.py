@@ -143,3 +143,26 @@ def test_ensemble_engine_equals_engines(dtype, res, B, M):
             assert np.array_equal(got[m], want), (dtype, res, n, m, np.abs(got[m] - want).max())
             del e
         assert len({got[m].tobytes() for m in range(M)}) == M     # the members differ
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_ensemble_fused_bn_maxpool_is_bitwise(dtype):
+    """The stem's BN + ReLU inside its max-pools for every member in one launch
+    (jr_bn_relu_maxpool3x3s2_fwd_grouped): predictions bitwise those of the
+    separate grouped apply + max-pool, full and partial batch."""
+    from jr import synth
+    from jr.ensemble import EnsembleEngine
+    from jr.inception import build_inception_v3
+    from jr.init import init_params
+    g = build_inception_v3(107, 107)
+    params = [init_params(g, 60 + m) for m in range(3)]
+    e = {f: EnsembleEngine(params, 6, 107, 107, dtype=dtype, fuse_pool=f) for f in (True, False)}
+    assert len(e[True].pool_fused) == 2 and not e[False].pool_fused
+    for n in (6, 4):
+        x = synth.fundus_batch(200, n, 107)
+        out = {}
+        for f, eng in e.items():
+            eng.set_batch(x)
+            eng.forward(n)
+            out[f] = eng.predictions(n)
+        assert np.array_equal(out[True], out[False]), (dtype, n)
