@@ -366,8 +366,8 @@ JR_API int jr_bn_relu_maxpool3x3s2_fwd_grouped(const jr_pool_desc* d, int dtype,
   int rc = check_pool(d, dtype, true);
   if (rc) return rc;
   if (!raw || !mean || !invstd || !beta || !y) return fail(JR_ERR_INVALID, "bn_relu_maxpool_fwd: null pointer");
-  if (images_per_member < 1 || stats_member_stride < 0 || beta_member_stride < 0)
-    return fail(JR_ERR_INVALID, "bn_relu_maxpool_fwd: bad member geometry");
+  if (images_per_member < 1 || d->n % images_per_member != 0 || stats_member_stride < 0 || beta_member_stride < 0)
+    return fail(JR_ERR_INVALID, "bn_relu_maxpool_fwd: images_per_member must divide n; strides >= 0");
   const int g = grid_for((int64_t)d->n * d->ho * d->wo * (d->c / 4));
   if (dtype == JR_F32)
     hipLaunchKernelGGL(k_bn_relu_maxpool_fwd<float>, dim3(g), dim3(256), 0, as_stream(stream), *d,
