@@ -234,6 +234,12 @@ class Engine:
             # per-lane scratch for the raw-output gradient of the launch in flight
             self.draw_lane = [self._t(max(B * u.ho * u.wo * u.cout for u in self.cunits), at)
                               for _ in range(self.nlanes)]
+            # the stem's filter gradients run on lane 1 beside its single-lane
+            # data-gradient chain: a second raw-gradient buffer for lane 0 (the
+            # next stem layer's BN backward must not overwrite what that
+            # filter gradient still reads)
+            self.draw_stem2 = (self._t(max(B * u.ho * u.wo * u.cout for u in self.cunits), at)
+                               if self.nlanes > 1 and not self.x8p else None)
             self.draw = self.draw_lane[0]
             self.dfeat = self._t(B * feat_c)
         if self.dt == _ffi.JR_BF16 or self.x8p:
@@ -249,6 +255,9 @@ class Engine:
             ws = max(ws, self.lib.jr_bn_workspace_size(B * u.ho * u.wo, u.cout))   # one backward per launch (or less)
         self.ws_bytes = int(ws)
         self.ws_lane = [self._t((self.ws_bytes + 15) // 4 + 4) for _ in range(self.nlanes)]
+        # the stem filter gradients' own workspace on lane 1
+        self.ws_stem = (self._t((self.ws_bytes + 15) // 4 + 4)
+                        if self.train_mode and getattr(self, "draw_stem2", None) is not None else None)
         self.ws = self.ws_lane[0]
 
     def _alloc_planes(self) -> None:
@@ -663,6 +672,14 @@ class Engine:
             add(bwd, L.jr_gap_bwd, (dt, self.dfeat.data_ptr(), B, ob.h * ob.w, ob.c, D(g.output_buf), s0),
                 "gap_bwd", 0, [("dfeat",)], d_all(g.output_buf))
             written = set()
+            readers: Dict[int, int] = {}
+            for q in g.nodes:
+                readers[q.x] = readers.get(q.x, 0) + 1
+            # the stem: the layers before the first buffer with several readers
+            stem_end = next((j for j, q in enumerate(g.nodes) if readers[q.x] > 1), 0)
+            stem_split = (nl > 1 and self.draw_stem2 is not None
+                          and os.environ.get("JR_STEM_WGRAD_LANE", "1") != "0")
+            sbuf = 0
             for i in range(len(g.nodes) - 1, -1, -1):
                 n = g.nodes[i]
                 ln = lane_of[i]
@@ -678,6 +695,13 @@ class Engine:
                     uid = u.first.idx
                     raw = self.raw_unit[uid].data_ptr()
                     draw = self.draw_lane[ln].data_ptr()
+                    dkey = ("draw", ln)
+                    wl = ln
+                    if stem_split and i < stem_end and ln == 0:   # filter gradient on lane 1
+                        if sbuf:
+                            draw, dkey = self.draw_stem2.data_ptr(), ("draw2", 0)
+                        sbuf ^= 1
+                        wl = 1
                     # one backward launch set for all members of the launch (segments:
                     # each member's upstream gradient slice, beta and dbeta)
                     for grp in self._bn_groups(u):
@@ -693,8 +717,7 @@ class Engine:
                                                           self.invstd_unit[uid].data_ptr() + 4 * co0, draw, ws, wsb,
                                                           s),
                             "bn_relu_bwd", ln, [("d", m.y.buf, m.y.c_off) for m, _ in grp] + [("r", uid), ("p",)],
-                            [("draw", ln), ("g", uid), ("ws", ln)], nbytes=3 * M * cg * self.esz)
-                    dkey = ("draw", ln)
+                            [dkey, ("g", uid), ("ws", ln)], nbytes=3 * M * cg * self.esz)
                     if x8p:             # the raw-output gradient as split planes (dgrad and wgrad operand)
                         drawp = self.drawp_lane[ln].data_ptr()
                         add(bwd, L.jr_split_x8p, (draw, M, u.cout, 0, u.cout, drawp, u.cout, 0, u.cout, M * u.cout, s),
@@ -702,9 +725,15 @@ class Engine:
                         draw, dkey = drawp, ("drawp", ln)
                     if uid in defer:
                         sg, _, nb = defer[uid]
-                        add(bwd, L.jr_conv2d_bwd_filter_slabs, (ctypes.byref(d), cdt, AX(u.x), draw, sg.slabs, nb, s),
-                            "conv_wgrad", ln, ax_reads(u.x) + [dkey], [("slab", uid)])
+                        add(bwd, L.jr_conv2d_bwd_filter_slabs, (ctypes.byref(d), cdt, AX(u.x), draw, sg.slabs, nb,
+                                                                S[wl]),
+                            "conv_wgrad", wl, ax_reads(u.x) + [dkey], [("slab", uid)])
                         pending.append((sg, uid))
+                    elif wl != ln:
+                        add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), cdt, AX(u.x), draw,
+                                                          self.grads.data_ptr() + 4 * u.koff,
+                                                          ctypes.c_void_p(self.ws_stem.data_ptr()), wsb, S[wl]),
+                            "conv_wgrad", wl, ax_reads(u.x) + [dkey], [("g", uid), ("wss",)])
                     else:
                         add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), cdt, AX(u.x), draw,
                                                           self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
