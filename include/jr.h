@@ -226,6 +226,18 @@ typedef struct jr_bn_seg {
 int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
                          int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd, void* dx,
                          void* ws, size_t ws_bytes, void* stream);
+/* The backward of a conv2d_bn layer whose output only a 3x3/2 max-pool reads
+ * (forward: jr_bn_relu_maxpool3x3s2_fwd): the max-pool backward writes dy
+ * (d's x slice, from the pooled gradient at d's y slice and the argmax) and
+ * adds the BN backward's reduction sums from the same registers, then the
+ * finalize and the dx pass run as in jr_bn_relu_bwd -- one read of dy fewer.
+ * x: the raw conv output [n*h*w] x x_c_stride (channels 0..d->c), dx: its
+ * gradient in that geometry; d->c a multiple of 4, <= 1024.  ws: at least
+ * jr_bn_relu_bwd_maxpool_workspace_size(d) bytes. */
+size_t jr_bn_relu_bwd_maxpool_workspace_size(const jr_pool_desc* d);
+int jr_bn_relu_bwd_maxpool(int dtype, const jr_pool_desc* d, const uint8_t* argmax, const void* pooled_dy, void* dy,
+                           const void* x, int32_t x_c_stride, const float* mean, const float* invstd,
+                           const float* beta, void* dx, float* dbeta, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- pooling (Keras MaxPooling2D((3,3),(2,2)) / AveragePooling2D((3,3),
  *      (1,1),'same') inside InceptionV3, train.py:129-130) ------------ */

@@ -625,3 +625,191 @@ JR_API int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, cons
   if (rc) return rc;
   return bn_bwd_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, dx, ws, ws_bytes, as_stream(stream));
 }
+
+// ---------------------------------------------------------------------------
+// The backward of a conv2d_bn layer whose output only a 3x3/2 max-pool reads
+// (the stem's conv2d_3 / conv2d_5; forward: jr_bn_relu_maxpool3x3s2_fwd).
+// k_maxpool_bwd_bn routes the pooled gradient to the layer's output exactly
+// as k_maxpool_bwd (2x2 input cells, windows summed from +0 in (oh, ow)
+// order, stored in the path dtype) and, holding each dy in registers, adds
+// the BN reduce's sums (sum dy', sum dy' xhat, fp64) of its channel quad
+// over every cell it visits; one partial per block and channel ([2][c][grid],
+// fixed order: deterministic) replaces k_bn_reduce's second read of dy.
+// k_bn_finalize and k_bn_relu_bwd_apply then run as for any layer.
+template <typename T>
+__global__ void __launch_bounds__(256) k_maxpool_bwd_bn(jr_pool_desc d, const uint8_t* __restrict__ argmax,
+                                                        const T* __restrict__ pdy, T* __restrict__ dy,
+                                                        const T* __restrict__ x, int xs, const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd,
+                                                        const float* __restrict__ beta, double* part) {
+  __shared__ double red[256][8];
+  const int c4 = d.c >> 2;
+  const int hc = (d.h + 1) >> 1, wc = (d.w + 1) >> 1;
+  const int total = d.n * hc * wc * c4;
+  const int stride = gridDim.x * blockDim.x;
+  const int q = (blockIdx.x * blockDim.x + threadIdx.x) % c4;   // fixed per thread: blockDim.x % c4 == 0
+  float mu[4], is[4], be[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    mu[l] = mean[q * 4 + l];
+    is[l] = invstd[q * 4 + l];
+    be[l] = beta[q * 4 + l];
+  }
+  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const int cell = e / c4;
+    const int cb = cell % wc;
+    const int t = cell / wc;
+    const int ca = t % hc;
+    const int b = t / hc;
+    uint32_t am[2][2];
+    float4 g[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int oh = ca - 1 + i, ow = cb - 1 + j;
+        am[i][j] = 0xffffffffu;
+        g[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (oh >= 0 && oh < d.ho && ow >= 0 && ow < d.wo) {
+          const int64_t op = ((int64_t)b * d.ho + oh) * d.wo + ow;
+          am[i][j] = *reinterpret_cast<const uint32_t*>(argmax + op * d.c + q * 4);
+          float v[4];
+          if constexpr (sizeof(T) == 4) {
+            const float4 f = *reinterpret_cast<const float4*>(pdy + op * d.y_c_stride + d.y_c_off + q * 4);
+            v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+          } else {
+            const uint2 u = *reinterpret_cast<const uint2*>(pdy + op * d.y_c_stride + d.y_c_off + q * 4);
+            v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+            v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+          }
+          g[i][j] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const int ih = 2 * ca + u, iw = 2 * cb + v;
+        if (ih >= d.h || iw >= d.w) continue;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int r = u + 2 - 2 * i, c = v + 2 - 2 * j;
+            if (r > 2 || c > 2) continue;
+            const float ga[4] = {g[i][j].x, g[i][j].y, g[i][j].z, g[i][j].w};
+#pragma unroll
+            for (int l = 0; l < 4; ++l)
+              if ((int)((am[i][j] >> (8 * l)) & 0xff) == r * 3 + c) acc[l] += ga[l];
+          }
+        }
+        const int64_t pix = ((int64_t)b * d.h + ih) * d.w + iw;
+        float xv[4];
+        T* p = dy + pix * d.x_c_stride + d.x_c_off + q * 4;
+        if constexpr (sizeof(T) == 4) {
+          *reinterpret_cast<float4*>(p) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+          const float4 f = *reinterpret_cast<const float4*>(x + pix * xs + q * 4);
+          xv[0] = f.x; xv[1] = f.y; xv[2] = f.z; xv[3] = f.w;
+        } else {
+          uint2 w;
+          w.x = (uint32_t)f2bf(acc[0]) | ((uint32_t)f2bf(acc[1]) << 16);
+          w.y = (uint32_t)f2bf(acc[2]) | ((uint32_t)f2bf(acc[3]) << 16);
+          *reinterpret_cast<uint2*>(p) = w;
+#pragma unroll
+          for (int l = 0; l < 4; ++l) acc[l] = bf2f(f2bf(acc[l]));   // the value k_bn_reduce would read
+          const uint2 xr = *reinterpret_cast<const uint2*>(x + pix * xs + q * 4);
+          xv[0] = __uint_as_float(xr.x << 16); xv[1] = __uint_as_float(xr.x & 0xffff0000u);
+          xv[2] = __uint_as_float(xr.y << 16); xv[3] = __uint_as_float(xr.y & 0xffff0000u);
+        }
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+          const float xh = bn_xhat(xv[l], mu[l], is[l]);
+          const float g2 = __fadd_rn(xh, be[l]) > 0.f ? acc[l] : 0.f;
+          s0[l] += (double)g2;
+          s1[l] += (double)g2 * (double)xh;
+        }
+      }
+    }
+  }
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    red[t][l] = s0[l];
+    red[t][4 + l] = s1[l];
+  }
+  __syncthreads();
+  // threads t, t + c4, t + 2 c4, ... hold the same channel quad: fixed-order sum
+  if (t < c4) {
+    double a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = red[t][k];
+    for (int o = t + c4; o < (int)blockDim.x; o += c4)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] += red[o][k];
+    const int64_t nch = gridDim.x;
+    const int qq = (blockIdx.x * blockDim.x + t) % c4;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      part[(int64_t)(qq * 4 + l) * nch + blockIdx.x] = a[l];
+      part[(int64_t)(d.c + qq * 4 + l) * nch + blockIdx.x] = a[4 + l];
+    }
+  }
+}
+
+JR_API size_t jr_bn_relu_bwd_maxpool_workspace_size(const jr_pool_desc* d) {
+  if (!d || d->c <= 0) return 0;
+  return (size_t)4096 * 2 * d->c * sizeof(double) + 2 * (size_t)d->c * sizeof(float);
+}
+
+JR_API int jr_bn_relu_bwd_maxpool(int dtype, const jr_pool_desc* d, const uint8_t* argmax, const void* pooled_dy,
+                                  void* dy, const void* x, int32_t x_c_stride, const float* mean,
+                                  const float* invstd, const float* beta, void* dx, float* dbeta, void* ws,
+                                  size_t ws_bytes, void* stream) {
+  if (!d || !argmax || !pooled_dy || !dy || !x || !mean || !invstd || !beta || !dx || !dbeta)
+    return fail(JR_ERR_INVALID, "bn_relu_bwd_maxpool: null pointer");
+  const int32_t c = d->c;
+  const int64_t m = (int64_t)d->n * d->h * d->w;
+  int rc = check_common(dtype, m, c);
+  if (rc) return rc;
+  if (c % 4 || c / 4 > 256) return fail(JR_ERR_UNSUPPORTED, "bn_relu_bwd_maxpool: c must be a multiple of 4, <= 1024");
+  if (d->h < 3 || d->w < 3 || d->ho != (d->h - 3) / 2 + 1 || d->wo != (d->w - 3) / 2 + 1)
+    return fail(JR_ERR_INVALID, "bn_relu_bwd_maxpool: the pool must be 3x3 stride 2 valid");
+  if (!check_slice(dtype, d->y_c_off, d->y_c_stride, c) || !check_slice(dtype, d->x_c_off, d->x_c_stride, c) ||
+      !check_slice(dtype, 0, x_c_stride, c))
+    return fail(JR_ERR_INVALID, "bn_relu_bwd_maxpool: bad slice");
+  if (!ws || ws_bytes < jr_bn_relu_bwd_maxpool_workspace_size(d))
+    return fail(JR_ERR_WORKSPACE, "bn_relu_bwd_maxpool: workspace too small");
+  hipStream_t s = as_stream(stream);
+  const int64_t cells = (int64_t)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2) * (c / 4);
+  const int bs = 256 / (c / 4) * (c / 4);        // a whole number of channel-quad rows per block
+  const int grid = (int)std::min<int64_t>(std::max<int64_t>(ceil_div(cells, bs), 1), 4096);
+  double* part = static_cast<double*>(ws);
+  float* k1 = reinterpret_cast<float*>(part + (size_t)grid * 2 * c);
+  float* k2 = k1 + c;
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_maxpool_bwd_bn<float>, dim3(grid), dim3(bs), 0, s, *d, argmax, (const float*)pooled_dy,
+                       (float*)dy, (const float*)x, x_c_stride, mean, invstd, beta, part);
+  else
+    hipLaunchKernelGGL(k_maxpool_bwd_bn<uint16_t>, dim3(grid), dim3(bs), 0, s, *d, argmax,
+                       (const uint16_t*)pooled_dy, (uint16_t*)dy, (const uint16_t*)x, x_c_stride, mean, invstd, beta,
+                       part);
+  rc = check_launch("maxpool_bwd + bn reduce");
+  if (rc) return rc;
+  BnSegs sg{};
+  sg.n = 1;
+  sg.dy[0] = static_cast<const char*>(dy) + (size_t)d->x_c_off * (dtype == JR_BF16 ? 2 : 4);
+  sg.dy_off[0] = 0;
+  sg.dy_stride[0] = d->x_c_stride;
+  sg.beta[0] = beta;
+  sg.dbeta[0] = dbeta;
+  sg.c0[0] = 0;
+  sg.c0[1] = c;
+  hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, grid, c, m, 0.f, k1, k2,
+                     sg);
+  rc = check_launch("bn_bwd finalize");
+  if (rc) return rc;
+  return bn_bwd_apply_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, k1, k2, dx, s);
+}

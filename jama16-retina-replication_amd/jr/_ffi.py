@@ -124,6 +124,10 @@ _SIGS = {
                                     c_void_p]),
     "jr_bn_relu_maxpool3x3s2_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_void_p]),
+    "jr_bn_relu_bwd_maxpool_workspace_size": (c_size_t, [POINTER(PoolDesc)]),
+    "jr_bn_relu_bwd_maxpool": (c_int, [c_int, POINTER(PoolDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                       c_void_p]),
     "jr_bn_relu_maxpool3x3s2_fwd_grouped": (c_int, [POINTER(PoolDesc), c_int, c_int32, c_void_p, c_void_p, c_void_p,
                                                     c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "jr_maxpool3x3s2_bwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p, c_int,
@@ -231,6 +235,7 @@ def call(name: str, *args) -> int:
     lib = load()
     rc = getattr(lib, name)(*args)
     if isinstance(rc, int) and name not in ("jr_conv2d_workspace_size", "jr_bn_workspace_size",
+                                            "jr_bn_relu_bwd_maxpool_workspace_size",
                                             "jr_conv2d_get_config", "jr_conv2d_num_configs", "jr_conv2d_config_generation",
                                             "jr_conv_weights_bf16_tiles"):
         check(name, rc)

@@ -253,6 +253,8 @@ class Engine:
             for op in (ops if self.train_mode else ops[:1]):
                 ws = max(ws, self.lib.jr_conv2d_workspace_size(ctypes.byref(d), op, self.cdt))
             ws = max(ws, self.lib.jr_bn_workspace_size(B * u.ho * u.wo, u.cout))   # one backward per launch (or less)
+        for i in self.pool_fused:                      # the fused max-pool + BN backward's partials
+            ws = max(ws, self.lib.jr_bn_relu_bwd_maxpool_workspace_size(ctypes.byref(self._pool_desc(g.nodes[i], B))))
         self.ws_bytes = int(ws)
         self.ws_lane = [self._t((self.ws_bytes + 15) // 4 + 4) for _ in range(self.nlanes)]
         # the stem filter gradients' own workspace on lane 1
@@ -672,6 +674,11 @@ class Engine:
             add(bwd, L.jr_gap_bwd, (dt, self.dfeat.data_ptr(), B, ob.h * ob.w, ob.c, D(g.output_buf), s0),
                 "gap_bwd", 0, [("dfeat",)], d_all(g.output_buf))
             written = set()
+            # fp32: the fused stem pools' backward carries the BN reduce
+            # (bf16 keeps the separate kernels, whose batch-of-rows fp32 sums
+            # it would not reproduce bit for bit)
+            pool_bwd = (self.pool_fused if dt == _ffi.JR_F32 and os.environ.get("JR_FUSE_POOL_BWD", "1") != "0"
+                        else {})
             readers: Dict[int, int] = {}
             for q in g.nodes:
                 readers[q.x] = readers.get(q.x, 0) + 1
@@ -704,7 +711,21 @@ class Engine:
                         wl = 1
                     # one backward launch set for all members of the launch (segments:
                     # each member's upstream gradient slice, beta and dbeta)
-                    for grp in self._bn_groups(u):
+                    pool_i = next((j for j, b in pool_bwd.items() if b == u.first.y.buf), None)
+                    if pool_i is not None:    # the max-pool backward adds the BN reduce's sums
+                        pn, m0 = g.nodes[pool_i], u.first
+                        pd = self._pool_desc(pn, B)
+                        keep.append(pd)
+                        add(bwd, L.jr_bn_relu_bwd_maxpool, (dt, ctypes.byref(pd), self.argmax[pool_i].data_ptr(),
+                                                            D(pn.y.buf), D(pn.x), raw, u.cout,
+                                                            self.mean_unit[uid].data_ptr(),
+                                                            self.invstd_unit[uid].data_ptr(),
+                                                            self._p(f"batch_normalization_{m0.idx + 1}/beta"), draw,
+                                                            self._gp(f"batch_normalization_{m0.idx + 1}/beta"), ws,
+                                                            wsb, s),
+                            "bn_relu_bwd", ln, [("d", pn.y.buf, pn.y.c_off), ("am", pool_i), ("r", uid), ("p",)],
+                            d_all(pn.x) + [dkey, ("g", uid), ("ws", ln)], nbytes=4 * M * u.cout * self.esz)
+                    for grp in ([] if pool_i is not None else self._bn_groups(u)):
                         co0 = grp[0][1]
                         cg = sum(m.cout for m, _ in grp)
                         segs = (_ffi.BnSeg * len(grp))(*[
@@ -750,6 +771,8 @@ class Engine:
                     if trigger:
                         flush()
                     bwd.append(Call("param_ready", u.koff, "hook", 0))
+                elif n.kind == "maxpool" and i in pool_bwd:
+                    continue            # with its producer's BN backward (jr_bn_relu_bwd_maxpool)
                 elif n.kind == "maxpool":
                     d = self._pool_desc(n, B)
                     keep.append(d)

@@ -18,7 +18,7 @@ def header_symbols(name="jr.h"):
 def test_header_declares_the_hot_path_surface():
     syms = header_symbols()
     for s in ("jr_conv2d_fwd", "jr_conv2d_bwd_data", "jr_conv2d_bwd_filter", "jr_bn_stats", "jr_bn_relu_apply",
-              "jr_bn_relu_bwd", "jr_maxpool3x3s2_fwd", "jr_bn_relu_maxpool3x3s2_fwd", "jr_bn_relu_maxpool3x3s2_fwd_grouped", "jr_avgpool3x3s1_bwd", "jr_gap_fwd", "jr_head_fwd",
+              "jr_bn_relu_bwd", "jr_maxpool3x3s2_fwd", "jr_bn_relu_maxpool3x3s2_fwd", "jr_bn_relu_bwd_maxpool", "jr_bn_relu_maxpool3x3s2_fwd_grouped", "jr_avgpool3x3s1_bwd", "jr_gap_fwd", "jr_head_fwd",
               "jr_head_bwd", "jr_nesterov_update", "jr_sgd_update", "jr_graph_begin", "jr_last_error"):
         assert s in syms
 
