@@ -58,7 +58,8 @@ typedef enum jr_status {
   JR_ERR_INVALID = -1,     /* bad argument / unsupported geometry          */
   JR_ERR_HIP = -2,         /* a HIP runtime call failed                    */
   JR_ERR_UNSUPPORTED = -3, /* valid request this build does not implement  */
-  JR_ERR_WORKSPACE = -4    /* workspace smaller than *_workspace_size      */
+  JR_ERR_WORKSPACE = -4,   /* workspace smaller than *_workspace_size      */
+  JR_ERR_DEVICE = -5       /* a kernel reported a device-side failure      */
 } jr_status;
 
 typedef enum jr_dtype { JR_F32 = 0, JR_BF16 = 1, JR_F32_X8 = 2, JR_F32_X8P = 3 } jr_dtype;
@@ -93,6 +94,19 @@ typedef struct jr_pool_desc {
 int jr_init(int device);
 const char* jr_last_error(void);
 const char* jr_version(void);
+/* Device-side failures of the launches on the CURRENT device since the last
+ * check (call it after synchronising the streams that ran them): JR_OK, or
+ * JR_ERR_DEVICE when a kernel counted a failure into the library's device
+ * error word -- today the stream-K hand-off of a conv GEMM whose owner block
+ * gave up waiting for a later piece's partial (its output is then invalid).
+ * On JR_ERR_DEVICE the call synchronises the device, re-zeroes every
+ * stream-K hand-off flag and the word, so the NEXT launches are correct.
+ * Host-synchronising (one 4-byte copy; the repair path a device sync). */
+int jr_device_check(void);
+/* Diagnostics: the stream-K owner's poll bound for later launches (default
+ * 2^22 polls, ~1 s; 0 = never wait, every unpublished partial is a failure).
+ * Process-wide. */
+int jr_debug_set_sk_spin_limit(uint32_t spins);
 
 /* ---- convolution (train.py:129-130 -> Keras Conv2D -> TF Conv2D,
  *      Conv2DBackpropInput, Conv2DBackpropFilter created by .minimize at
@@ -394,6 +408,9 @@ int jr_graph_begin(void* stream);
 int jr_graph_end(void* stream, void** graph_exec);
 int jr_graph_launch(void* graph_exec, void* stream);
 int jr_graph_destroy(void* graph_exec);
+/* Device regions the library allocated for a capture (stream-K hand-off
+ * flags of captured conv GEMMs) and released by jr_graph_destroy (tests). */
+int jr_graph_regions(void* graph_exec);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,9 @@
-// jr_api.cpp — library-level C-ABI: init, launch-error mapping, HIP graph
-// capture (the error convention itself is host-only code: jr_error.cpp).
+// jr_api.cpp — library-level C-ABI: init, launch-error mapping, the device
+// error word, HIP graph capture (the error convention itself is host-only
+// code: jr_error.cpp).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -19,7 +21,16 @@ struct Scratch {
 };
 std::mutex g_scratch_mu;
 std::map<std::tuple<int, hipStream_t, int>, Scratch> g_scratch;
-std::vector<unsigned*> g_scratch_kept;   // outgrown / captured regions: launches in flight may still use them
+std::vector<unsigned*> g_scratch_kept;   // outgrown regions: launches in flight may still use them
+// regions handed to a capturing stream, per capture sequence id until
+// jr_graph_end moves them to the graph exec that references them (freed by
+// jr_graph_destroy; ADVICE r04: they used to be kept forever)
+std::map<unsigned long long, std::vector<void*>> g_capture_regions;
+std::map<hipGraphExec_t, std::vector<void*>> g_graph_regions;
+
+constexpr int kMaxDevices = 64;
+unsigned* g_err_word[kMaxDevices] = {};
+std::atomic<unsigned> g_sk_spins{1u << 22};
 
 unsigned* scratch_alloc(hipStream_t s, size_t words) {
   void* p = nullptr;
@@ -27,13 +38,33 @@ unsigned* scratch_alloc(hipStream_t s, size_t words) {
   if (hipMemsetAsync(p, 0, words * sizeof(unsigned), s) != hipSuccess) return nullptr;
   return static_cast<unsigned*>(p);
 }
+
+bool capturing(hipStream_t s, unsigned long long* id) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long cid = 0;
+  if (hipStreamGetCaptureInfo(s, &cs, &cid) != hipSuccess) return false;
+  if (id) *id = cid;
+  return cs != hipStreamCaptureStatusNone;
+}
+
+// allocate + zero the current device's error word (not under capture)
+int err_word_init(int dev) {
+  if (dev < 0 || dev >= kMaxDevices) return fail(JR_ERR_UNSUPPORTED, "libjr: device ordinal above 63");
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  if (g_err_word[dev]) return JR_OK;
+  void* p = nullptr;
+  if (hipMalloc(&p, sizeof(unsigned)) != hipSuccess || hipMemset(p, 0, sizeof(unsigned)) != hipSuccess)
+    return fail(JR_ERR_HIP, "libjr: device error word could not be allocated");
+  g_err_word[dev] = static_cast<unsigned*>(p);
+  return JR_OK;
+}
 }  // namespace
 
 unsigned* stream_scratch(hipStream_t s, int kind, size_t words) {
   words = std::max<size_t>(words, 1);
   std::lock_guard<std::mutex> lk(g_scratch_mu);
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+  unsigned long long cid = 0;
+  if (capturing(s, &cid)) {
     // (the zeroing memset becomes a node of the graph ahead of the kernel;
     // the kernel leaves the words zero, so every replay starts from zero;
     // hipMalloc is not a stream operation: relaxed mode lets it through)
@@ -42,10 +73,10 @@ unsigned* stream_scratch(hipStream_t s, int kind, size_t words) {
     void* raw = nullptr;
     const bool ok = hipMalloc(&raw, words * sizeof(unsigned)) == hipSuccess;
     (void)hipThreadExchangeStreamCaptureMode(&mode);
-    unsigned* p = ok && hipMemsetAsync(raw, 0, words * sizeof(unsigned), s) == hipSuccess
-                      ? static_cast<unsigned*>(raw) : nullptr;
-    if (p) g_scratch_kept.push_back(p);
-    return p;
+    if (!ok) return nullptr;
+    g_capture_regions[cid].push_back(raw);
+    return hipMemsetAsync(raw, 0, words * sizeof(unsigned), s) == hipSuccess ? static_cast<unsigned*>(raw)
+                                                                              : nullptr;
   }
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
@@ -61,6 +92,19 @@ unsigned* stream_scratch(hipStream_t s, int kind, size_t words) {
   return e.p;
 }
 
+unsigned* device_error_word() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    if (g_err_word[dev]) return g_err_word[dev];
+  }
+  if (capturing(nullptr, nullptr)) return nullptr;   // (jr_init allocates it before any capture)
+  return err_word_init(dev) == JR_OK ? g_err_word[dev] : nullptr;
+}
+
+unsigned sk_spin_limit() { return g_sk_spins.load(std::memory_order_relaxed); }
+
 int check_launch(const char* what) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(JR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -71,7 +115,7 @@ int check_launch(const char* what) {
 
 using namespace jr;
 
-JR_API const char* jr_version(void) { return "libjr 0.2 gfx950 (implicit-GEMM conv: fp32 x8-split / fp32 / bf16 MFMA)"; }
+JR_API const char* jr_version(void) { return "libjr 0.3 gfx950 (implicit-GEMM conv: fp32 x8-split / fp32 / bf16 MFMA)"; }
 
 JR_API int jr_init(int device) {
   int n = 0;
@@ -85,6 +129,42 @@ JR_API int jr_init(int device) {
   if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("jr_init: ") + hipGetErrorString(e));
   if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
     return fail(JR_ERR_UNSUPPORTED, std::string("jr_init: libjr is built for gfx950, device is ") + prop.gcnArchName);
+  return err_word_init(device);
+}
+
+JR_API int jr_device_check(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
+    return fail(JR_ERR_HIP, "jr_device_check: no current device");
+  unsigned* w = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    w = g_err_word[dev];
+  }
+  if (!w) return JR_OK;                 // nothing has run on this device yet
+  unsigned h = 0;
+  hipError_t e = hipMemcpy(&h, w, sizeof(unsigned), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("jr_device_check: ") + hipGetErrorString(e));
+  if (h == 0) return JR_OK;
+  // repair: every launch (and every late publisher) has finished, then the
+  // hand-off flags of every stream of this device and the word go back to 0
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("jr_device_check: ") + hipGetErrorString(e));
+  {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (auto& kv : g_scratch)
+      if (std::get<0>(kv.first) == dev && std::get<2>(kv.first) == 0 && kv.second.p)
+        (void)hipMemset(kv.second.p, 0, kv.second.words * sizeof(unsigned));
+  }
+  (void)hipMemset(w, 0, sizeof(unsigned));
+  (void)hipDeviceSynchronize();
+  return fail(JR_ERR_DEVICE, "stream-K hand-off: " + std::to_string(h) +
+                                 " partial tile(s) not published within the owner's poll bound; the outputs of the "
+                                 "launches since the last jr_device_check are invalid (hand-off flags reset)");
+}
+
+JR_API int jr_debug_set_sk_spin_limit(uint32_t spins) {
+  g_sk_spins.store(spins, std::memory_order_relaxed);
   return JR_OK;
 }
 
@@ -96,13 +176,35 @@ JR_API int jr_graph_begin(void* stream) {
 
 JR_API int jr_graph_end(void* stream, void** graph_exec) {
   if (!graph_exec) return fail(JR_ERR_INVALID, "graph_end: null output");
+  unsigned long long cid = 0;
+  const bool cap = capturing(as_stream(stream), &cid);
+  std::vector<void*> regions;
+  auto take_regions = [&] {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    auto it = g_capture_regions.find(cid);
+    if (cap && it != g_capture_regions.end()) {
+      regions.swap(it->second);
+      g_capture_regions.erase(it);
+    }
+  };
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamEndCapture(as_stream(stream), &g);
-  if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("graph_end: ") + hipGetErrorString(e));
+  take_regions();
+  if (e != hipSuccess) {
+    for (void* p : regions) (void)hipFree(p);
+    return fail(JR_ERR_HIP, std::string("graph_end: ") + hipGetErrorString(e));
+  }
   hipGraphExec_t ex = nullptr;
   e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
-  if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("graph_instantiate: ") + hipGetErrorString(e));
+  if (e != hipSuccess) {
+    for (void* p : regions) (void)hipFree(p);
+    return fail(JR_ERR_HIP, std::string("graph_instantiate: ") + hipGetErrorString(e));
+  }
+  if (!regions.empty()) {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    g_graph_regions[ex] = std::move(regions);
+  }
   *graph_exec = reinterpret_cast<void*>(ex);
   return JR_OK;
 }
@@ -116,7 +218,28 @@ JR_API int jr_graph_launch(void* graph_exec, void* stream) {
 
 JR_API int jr_graph_destroy(void* graph_exec) {
   if (!graph_exec) return JR_OK;
-  const hipError_t e = hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(graph_exec));
+  const hipGraphExec_t ex = reinterpret_cast<hipGraphExec_t>(graph_exec);
+  const hipError_t e = hipGraphExecDestroy(ex);
+  std::vector<void*> regions;
+  {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    auto it = g_graph_regions.find(ex);
+    if (it != g_graph_regions.end()) {
+      regions.swap(it->second);
+      g_graph_regions.erase(it);
+    }
+  }
+  if (!regions.empty()) {
+    // replays of the destroyed exec may still be in flight: hipFree waits for
+    // the device before releasing
+    for (void* p : regions) (void)hipFree(p);
+  }
   if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("graph_destroy: ") + hipGetErrorString(e));
   return JR_OK;
+}
+
+JR_API int jr_graph_regions(void* graph_exec) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  auto it = g_graph_regions.find(reinterpret_cast<hipGraphExec_t>(graph_exec));
+  return it == g_graph_regions.end() ? 0 : (int)it->second.size();
 }

@@ -22,6 +22,13 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // call: graph replays may run on any stream.  nullptr if allocation failed.
 unsigned* stream_scratch(hipStream_t s, int kind, size_t words);
 
+// The current device's error word (jr_api.cpp): kernels count device-side
+// failures into it (vector atomics); jr_device_check() reads, reports and
+// clears it.  Allocated by jr_init (or on first use outside a capture).
+unsigned* device_error_word();
+// Stream-K owner poll bound (jr_debug_set_sk_spin_limit; default 2^22).
+unsigned sk_spin_limit();
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Bijective XCD-aware remap of a flat workgroup id (cdna_hip_programming.md

@@ -1094,6 +1094,10 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     a.sk_flags = stream_scratch(s, 0, (size_t)p.sk_blocks * members);
     if (!a.sk_flags) return fail(JR_ERR_HIP, "conv: stream-K flag words could not be allocated");
     a.sk_fmb = (long long)p.sk_blocks * sizeof(unsigned);
+    // a timed-out owner counts itself here instead of adding an unpublished slot
+    a.sk_err = device_error_word();
+    if (!a.sk_err) return fail(JR_ERR_HIP, "conv: no device error word (call jr_init before capturing)");
+    a.sk_spins = sk_spin_limit();
     grid = dim3(p.sk_blocks, members, 1);
   }
   if (is_halo(dtype, p.tile)) {

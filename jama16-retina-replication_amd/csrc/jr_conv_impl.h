@@ -53,6 +53,10 @@ struct ConvArgs {
   long long sk_ipb, sk_mb, sk_fmb;
   unsigned* sk_flags;
   float* sk_part;
+  // the library's device error word (jr_device_check) and the owner's poll
+  // bound (jr_debug_set_sk_spin_limit; 0 = never wait)
+  unsigned* sk_err;
+  unsigned sk_spins;
 };
 
 // Moves a grouped GEMM's operand / output pointers to member blockIdx.y
@@ -195,19 +199,37 @@ __device__ __forceinline__ void sk_publish(const ConvArgs& g, const f32x16 (&acc
     __hip_atomic_store(g.sk_flags + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// acc += the partial of block b (published by sk_publish), after its flag
+// acc += the partial of block b (published by sk_publish), after its flag.
+// ONE lane polls ONE word, relaxed, at most g.sk_spins times (~1 s at the
+// default).  Seen: the flag is zeroed again (this block is its only reader)
+// and the partial added.  Not seen: nothing is added, the flag is left alone
+// (its late publisher may still set it) and the library's device error word
+// g.sk_err counts the failure -- jr_device_check() reports it as
+// JR_ERR_DEVICE and re-zeroes every hand-off flag, so a timed-out launch
+// yields an error, never numbers, and never poisons a later launch.
 template <int TM, int TN, int NW = 4>
 __device__ __forceinline__ void sk_absorb(const ConvArgs& g, f32x16 (&acc)[TM][TN], int b, int wave, int lane) {
   constexpr int SLOT = NW * TM * TN * 16 * 64;
-  if (threadIdx.x == 0) {            // ONE lane polls ONE word, relaxed; bounded (~1 s), then gives up
-    for (unsigned spins = 0; spins < (1u << 22); ++spins) {
-      if (__hip_atomic_load(g.sk_flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) break;
+  __shared__ int s_seen;
+  if (threadIdx.x == 0) {
+    int seen = 0;
+    for (unsigned spins = 0; spins < g.sk_spins; ++spins) {
+      if (__hip_atomic_load(g.sk_flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
+        seen = 1;
+        break;
+      }
       __builtin_amdgcn_s_sleep(2);
     }
-    // the only reader of flag b: zero again for the stream's next launch
-    __hip_atomic_store(g.sk_flags + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seen)
+      __hip_atomic_store(g.sk_flags + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __hip_atomic_fetch_add(g.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_seen = seen;
   }
   __syncthreads();
+  const int ok = s_seen;
+  __syncthreads();                     // every wave has read s_seen before the next absorb writes it
+  if (!ok) return;                     // (uniform)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below the poll)
   const auto rs = sk_rsrc(g.sk_part + (long long)b * SLOT);
   typedef int i32x4 __attribute__((ext_vector_type(4)));

@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("JR_LIB", os.path.join(_HERE, "libjr.so"))
 
 JR_OK = 0
+JR_ERR_DEVICE = -5   # jr_device_check: a kernel reported a device-side failure
 JR_F32 = 0
 JR_BF16 = 1
 JR_F32_X8 = 2      # conv entry points only: fp32 tensors, bf16x8-split MFMA products (jr.h)
@@ -161,6 +162,9 @@ _SIGS = {
     "jr_graph_end": (c_int, [c_void_p, POINTER(c_void_p)]),
     "jr_graph_launch": (c_int, [c_void_p, c_void_p]),
     "jr_graph_destroy": (c_int, [c_void_p]),
+    "jr_graph_regions": (c_int, [c_void_p]),
+    "jr_device_check": (c_int, []),
+    "jr_debug_set_sk_spin_limit": (c_int, [ctypes.c_uint32]),
 }
 
 EXPORTED = tuple(_SIGS)
@@ -229,6 +233,14 @@ def last_error() -> str:
 def check(name: str, rc: int) -> None:
     if rc != JR_OK:
         raise JRError(name, rc, last_error())
+
+
+def device_check() -> None:
+    """jr_device_check on the current device (after the caller synchronised
+    its streams): raise JRError when a launch reported a device-side failure
+    (a stream-K hand-off that timed out); the library has then reset its
+    hand-off flags, so later launches are correct again."""
+    check("jr_device_check", load().jr_device_check())
 
 
 def call(name: str, *args) -> int:

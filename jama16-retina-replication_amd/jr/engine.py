@@ -949,8 +949,12 @@ class Engine:
         _ffi.check("jr_graph_launch", self.lib.jr_graph_launch(ctypes.c_void_p(self._graphs[B]), self._s))
 
     def synchronize(self) -> None:
+        """Wait for every lane, then jr_device_check: a device-side failure
+        of any launch since the last check (a stream-K hand-off that timed
+        out) raises JRError here instead of leaving wrong numbers."""
         for st in self.lane_streams:
             st.synchronize()
+        _ffi.device_check()
 
     def loss_value(self) -> float:
         self.synchronize()

@@ -32,6 +32,7 @@ import torch
 from . import _ffi
 from .engine import DTYPES, fusable_pools, pinned_tile_table
 from .inception import BN_EPS, build_inception_v3
+from .lanes import Call, node_lanes, schedule
 from .plan import build_plan
 
 
@@ -40,7 +41,7 @@ class EnsembleEngine:
 
     def __init__(self, params: List[np.ndarray], batch: int, height: int = 299, width: int = 299, units: int = 1,
                  device: int | torch.device = 0, dtype: str = "f32", conv_math: Optional[str] = None,
-                 tiles: str = "pinned", head: str = "sigmoid", fuse_pool: Optional[bool] = None):
+                 tiles: str = "pinned", head: str = "sigmoid", fuse_pool: Optional[bool] = None, lanes: int = 1):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if conv_math is None:
@@ -72,6 +73,14 @@ class EnsembleEngine:
         self.head_mode = _ffi.JR_HEAD_SIGMOID if head == "sigmoid" else _ffi.JR_HEAD_SOFTMAX
         self.stream = torch.cuda.Stream(device=self.device)
         self._s = ctypes.c_void_p(self.stream.cuda_stream)
+        # branch lanes (jr.lanes, as jr.Engine): lane 0 is self.stream; every
+        # lane has its OWN conv workspace (split-K slabs, stream-K partial
+        # slots, statistics partials), declared as the resource ("ws", lane)
+        self.nlanes = max(1, int(lanes))
+        self.lane_streams = [self.stream] + [torch.cuda.Stream(device=self.device) for _ in range(1, self.nlanes)]
+        self._fork_ev = torch.cuda.Event()
+        self._join_ev = [torch.cuda.Event() for _ in range(self.nlanes - 1)]
+        self._tail_ev = [torch.cuda.Event() for _ in range(self.nlanes)]
         self._alloc()
         self.load_params(params)
         self.tiles = "heuristic"
@@ -138,7 +147,8 @@ class EnsembleEngine:
             d = self._conv_desc(u, B)
             ws = max(ws, self.lib.jr_conv2d_workspace_size_grouped(ctypes.byref(d), self.cdt, M))
         self.ws_bytes = int(ws)
-        self.ws = self._t((self.ws_bytes + 15) // 4 + 4)
+        self.ws_lane = [self._t((self.ws_bytes + 15) // 4 + 4) for _ in range(self.nlanes)]
+        self.ws = self.ws_lane[0]
 
     def load_params(self, params: List[np.ndarray]) -> None:
         """Keras-layout flat parameters of every member (jr.checkpoint.load)."""
@@ -182,12 +192,27 @@ class EnsembleEngine:
             return self._calls[B]
         if B > self.batch or B <= 0:
             raise ValueError(f"batch {B} outside 1..{self.batch}")
-        L, g, M, s = self.lib, self.g, self.members, self._s
+        L, g, M, nl = self.lib, self.g, self.members, self.nlanes
+        S = [ctypes.c_void_p(st.cuda_stream) for st in self.lane_streams]
+        WS = [ctypes.c_void_p(w.data_ptr()) for w in self.ws_lane]
+        wsb = ctypes.c_size_t(self.ws_bytes)
+        lane_of = node_lanes(g, self.plan, nl)
         calls, keep = [], []
+
+        def add(fn, args, name, lane, reads, writes):
+            calls.append(Call(fn, args, name, lane, tuple(reads), tuple(writes)))
+
+        # resources (jr.lanes.schedule), as jr.Engine: activation channel
+        # slices, a launch's raw output + statistics, the lane's workspace
+        slices = {g.input_buf: {0}}
+        for n in g.nodes:
+            slices.setdefault(n.y.buf, set()).add(n.y.c_off)
+        a_all = lambda b: [("a", b, o) for o in sorted(slices[b])]  # noqa: E731
         A = lambda bid: self.acts[bid].data_ptr()  # noqa: E731
-        ws, wsb = ctypes.c_void_p(self.ws.data_ptr()), ctypes.c_size_t(self.ws_bytes)
         fused_bufs = set(self.pool_fused.values())
         for i, n in enumerate(g.nodes):
+            ln = lane_of[i]
+            s = S[ln]
             if n.kind == "conv":
                 u = self.plan.unit_of[n.idx]
                 if u.first is not n:
@@ -203,19 +228,19 @@ class EnsembleEngine:
                 raw = self.raw_unit[uid].data_ptr()
                 mean = self.stats.data_ptr() + 4 * so
                 inv = mean + 4 * u.cout
-                calls.append((L.jr_conv2d_fwd_bn_stats_grouped,
-                              (ctypes.byref(d), self.cdt, M, A(u.x), self.act_ms[u.x], w, w_ms, raw,
-                               self.raw_ms[uid], BN_EPS, mean, inv, self.stats_ms, ws, wsb, s), "conv_fwd"))
+                add(L.jr_conv2d_fwd_bn_stats_grouped,
+                    (ctypes.byref(d), self.cdt, M, A(u.x), self.act_ms[u.x], w, w_ms, raw, self.raw_ms[uid], BN_EPS,
+                     mean, inv, self.stats_ms, WS[ln], wsb, s), "conv_fwd", ln, a_all(u.x), [("r", uid), ("ws", ln)])
                 rows = B * u.ho * u.wo
                 for mem, co in zip(u.members, u.col_off):
                     if mem.y.buf in fused_bufs:
                         continue        # applied inside its max-pool
                     yb = g.bufs[mem.y.buf]
-                    calls.append((L.jr_bn_relu_apply_grouped,
-                                  (self.dt, M, raw, co, u.cout, self.raw_ms[uid], rows, mem.cout, mean + 4 * co,
-                                   inv + 4 * co, self.stats_ms, self._p(0, f"batch_normalization_{mem.idx + 1}/beta"),
-                                   self.nparam, A(mem.y.buf), mem.y.c_off, yb.c, self.act_ms[mem.y.buf], s),
-                                  "bn_relu"))
+                    add(L.jr_bn_relu_apply_grouped,
+                        (self.dt, M, raw, co, u.cout, self.raw_ms[uid], rows, mem.cout, mean + 4 * co, inv + 4 * co,
+                         self.stats_ms, self._p(0, f"batch_normalization_{mem.idx + 1}/beta"), self.nparam,
+                         A(mem.y.buf), mem.y.c_off, yb.c, self.act_ms[mem.y.buf], s), "bn_relu", ln,
+                        [("r", uid)], [("a", mem.y.buf, mem.y.c_off)])
             else:
                 # pools: the member-major buffers of a full batch are one
                 # batch of M * B images (one launch); a partial last batch
@@ -227,36 +252,41 @@ class EnsembleEngine:
                     keep.append(d)
                     xi = A(n.x) + self.esz * m * self.act_ms[n.x]
                     yo = A(n.y.buf) + self.esz * m * self.act_ms[n.y.buf]
+                    out = [("a", n.y.buf, n.y.c_off)]
                     if i in self.pool_fused:    # BN + ReLU of the producing layer on the fly
                         pn = next(q for q in g.nodes if q.y.buf == n.x)
                         puid = self.plan.unit_of[pn.idx].first.idx
                         so = self.stat_off[puid]
                         mean = self.stats.data_ptr() + 4 * (so + m * self.stats_ms)
-                        calls.append((L.jr_bn_relu_maxpool3x3s2_fwd_grouped,
-                                      (ctypes.byref(d), self.dt, B, self.raw_unit[puid].data_ptr()
-                                       + self.esz * m * self.raw_ms[puid], mean, mean + 4 * pn.cout, self.stats_ms,
-                                       self._p(m, f"batch_normalization_{pn.idx + 1}/beta"), self.nparam, yo, None, s),
-                                      "bn_relu_maxpool_fwd"))
+                        add(L.jr_bn_relu_maxpool3x3s2_fwd_grouped,
+                            (ctypes.byref(d), self.dt, B, self.raw_unit[puid].data_ptr()
+                             + self.esz * m * self.raw_ms[puid], mean, mean + 4 * pn.cout, self.stats_ms,
+                             self._p(m, f"batch_normalization_{pn.idx + 1}/beta"), self.nparam, yo, None, s),
+                            "bn_relu_maxpool_fwd", ln, [("r", puid)], out)
                     elif n.kind == "maxpool":
-                        calls.append((L.jr_maxpool3x3s2_fwd, (ctypes.byref(d), self.dt, xi, yo, None, s),
-                                      "maxpool_fwd"))
+                        add(L.jr_maxpool3x3s2_fwd, (ctypes.byref(d), self.dt, xi, yo, None, s), "maxpool_fwd", ln,
+                            a_all(n.x), out)
                     else:
-                        calls.append((L.jr_avgpool3x3s1_fwd, (ctypes.byref(d), self.dt, xi, yo, s), "avgpool_fwd"))
+                        add(L.jr_avgpool3x3s1_fwd, (ctypes.byref(d), self.dt, xi, yo, s), "avgpool_fwd", ln,
+                            a_all(n.x), out)
         ob = g.bufs[g.output_buf]
+        s0 = S[0]
         if B == self.batch:
-            calls.append((L.jr_gap_fwd, (self.dt, A(g.output_buf), M * B, ob.h * ob.w, ob.c, self.feat.data_ptr(),
-                                         s), "gap_fwd"))
+            add(L.jr_gap_fwd, (self.dt, A(g.output_buf), M * B, ob.h * ob.w, ob.c, self.feat.data_ptr(), s0),
+                "gap_fwd", 0, a_all(g.output_buf), [("feat",)])
         else:
             for m in range(M):
-                calls.append((L.jr_gap_fwd, (self.dt, A(g.output_buf) + self.esz * m * self.act_ms[g.output_buf], B,
-                                             ob.h * ob.w, ob.c, self.feat.data_ptr() + 4 * m * self.batch * ob.c, s),
-                              "gap_fwd"))
+                add(L.jr_gap_fwd, (self.dt, A(g.output_buf) + self.esz * m * self.act_ms[g.output_buf], B,
+                                   ob.h * ob.w, ob.c, self.feat.data_ptr() + 4 * m * self.batch * ob.c, s0),
+                    "gap_fwd", 0, a_all(g.output_buf), [("feat",)])
         for m in range(M):
             f = self.feat.data_ptr() + 4 * m * self.batch * ob.c
             o = 4 * m * self.batch * self.units
-            calls.append((L.jr_head_fwd, (self.head_mode, f, self._p(m, "dense/kernel"), self._p(m, "dense/bias"),
-                                          self.labels.data_ptr(), B, ob.c, self.units, self.logits.data_ptr() + o,
-                                          self.probs.data_ptr() + o, self.loss.data_ptr() + 16 * m, s), "head_fwd"))
+            add(L.jr_head_fwd, (self.head_mode, f, self._p(m, "dense/kernel"), self._p(m, "dense/bias"),
+                                self.labels.data_ptr(), B, ob.c, self.units, self.logits.data_ptr() + o,
+                                self.probs.data_ptr() + o, self.loss.data_ptr() + 16 * m, s0), "head_fwd", 0,
+                [("feat",)], [("head",)])
+        schedule(calls)
         self._calls[B] = (calls, keep)
         return self._calls[B]
 
@@ -293,14 +323,26 @@ class EnsembleEngine:
 
     def forward(self, B: Optional[int] = None) -> None:
         calls, _ = self._build_calls(B or self.batch)
-        with torch.cuda.stream(self.stream):
-            for fn, args, name in calls:
-                rc = fn(*args)
-                if rc:
-                    raise _ffi.JRError(name, rc, _ffi.last_error())
+        if self.nlanes > 1:          # fork: every lane after the batch upload on lane 0
+            self._fork_ev.record(self.stream)
+            for st in self.lane_streams[1:]:
+                st.wait_event(self._fork_ev)
+        for c in calls:
+            st = self.lane_streams[c.lane]
+            for lj in c.waits:       # the other lane's tail (jr.lanes.schedule)
+                ev = self._tail_ev[lj]
+                ev.record(self.lane_streams[lj])
+                st.wait_event(ev)
+            rc = c.fn(*c.args)
+            if rc:
+                raise _ffi.JRError(c.name, rc, _ffi.last_error())
+        for ev, st in zip(self._join_ev, self.lane_streams[1:]):    # join onto lane 0
+            ev.record(st)
+            self.stream.wait_event(ev)
 
     def synchronize(self) -> None:
         self.stream.synchronize()
+        _ffi.device_check()          # (jr.Engine.synchronize: device-side failures raise)
 
     def predictions(self, n: Optional[int] = None) -> np.ndarray:
         """[members, n, units] sigmoid (softmax) outputs of the last forward."""

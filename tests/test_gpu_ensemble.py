@@ -166,3 +166,60 @@ def test_ensemble_fused_bn_maxpool_is_bitwise(dtype):
             eng.forward(n)
             out[f] = eng.predictions(n)
         assert np.array_equal(out[True], out[False]), (dtype, n)
+
+
+def test_ensemble_ten_members_grouped_equals_engines():
+    """BASELINE config 4's member count: ten members in
+    one EnsembleEngine at 107^2, bitwise ten jr.Engine(train=False), full and
+    partial batch."""
+    from jr import synth
+    from jr.engine import Engine
+    from jr.ensemble import EnsembleEngine
+    from jr.inception import build_inception_v3
+    from jr.init import init_params
+    res, B, M = 107, 8, 10
+    g = build_inception_v3(res, res)
+    params = [init_params(g, 300 + m) for m in range(M)]
+    ens = EnsembleEngine(params, B, res, res, dtype="f32")
+    e = Engine(B, res, res, dtype="f32", train=False, seed=0)
+    for n in (B, 3):
+        x = synth.fundus_batch(500 + n, n, res)
+        ens.set_batch(x)
+        ens.forward(n)
+        got = ens.predictions(n)
+        for m in range(M):
+            e.load_params(params[m])
+            e.set_batch(x)
+            e.forward(n)
+            assert np.array_equal(got[m], e.predictions(n)), (n, m)
+        assert len({got[m].tobytes() for m in range(M)}) == M
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("res,B", [(107, 8), (299, 32)])
+def test_ensemble_lanes_are_bitwise_one_lane(dtype, res, B):
+    """EnsembleEngine on two branch lanes, each with its own conv workspace
+    (split-K slabs, stream-K partials, statistics partials: the resource
+    ("ws", lane)): every pass bitwise the one-lane predictions, full and
+    partial batch (the round-4 prototype shared one workspace between the
+    lanes, tools/ensemble_lanes_race.py)."""
+    from jr import synth
+    from jr.ensemble import EnsembleEngine
+    from jr.inception import build_inception_v3
+    from jr.init import init_params
+    from jr.lanes import check_schedule
+    g = build_inception_v3(res, res)
+    params = [init_params(g, 80 + m) for m in range(3)]
+    one = EnsembleEngine(params, B, res, res, dtype=dtype, lanes=1)
+    two = EnsembleEngine(params, B, res, res, dtype=dtype, lanes=2)
+    assert one.tiles == two.tiles
+    for n in (B, 5):
+        calls, _ = two._build_calls(n)
+        check_schedule(calls)
+        assert {c.lane for c in calls} == {0, 1}
+        for k in range(3):
+            x = synth.fundus_batch(700 + 40 * k, n, res)
+            for e in (one, two):
+                e.set_batch(x)
+                e.forward(n)
+            assert np.array_equal(one.predictions(n), two.predictions(n)), (dtype, res, n, k)

@@ -69,13 +69,18 @@ def test_inputs_match_the_fixture(evalset):
     assert np.array_equal(np.vstack(ys), G["labels"])
 
 
+@pytest.mark.parametrize("grouped", [True, False], ids=["grouped", "per_member"])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_config4_ensemble_vs_fp64(evalset, dtype):
+def test_config4_ensemble_vs_fp64(evalset, dtype, grouped):
+    """grouped=True is evaluate.py's default path (one jr.ensemble.
+    EnsembleEngine for every member); per_member is
+    --per_member (one jr.Engine each)."""
     import evaluate
     from jr import checkpoint
     data, paths, _ = evalset
-    engines = evaluate.make_engines(paths, checkpoint.read_meta(paths[0]), B, dtype=dtype)
-    assert all(e.tiles == "pinned" for e in engines), [e.tiles for e in engines]
+    engines = evaluate.make_engines(paths, checkpoint.read_meta(paths[0]), B, dtype=dtype, grouped=grouped)
+    tiles = [engines.tiles] if grouped else [e.tiles for e in engines]
+    assert all(t == "pinned" for t in tiles), tiles
     preds, labels, ids = evaluate.predict_all(engines, data, B)
     assert ids == list(range(len(ids))) and labels.shape == G["labels"].shape
     assert np.array_equal(labels, G["labels"])
@@ -132,4 +137,12 @@ def test_cli_two_ranks_equal_one_rank(evalset):
                        and not ln.startswith("[Gloo]") and ln.strip()]
     assert strip(out1) == strip(out2), (out1, out2)
     assert open(one_csv).read() == open(two_csv).read()
-    assert "AUC:" in out1
+    # the default (grouped) CLI against the fp64 fixture: the printed AUC to
+    # 3 decimals (north_star) and the confusion matrix at the operating point
+    import re
+    auc = float(re.search(r"AUC:\s*([0-9.eE+-]+)", out1).group(1))
+    assert round(auc, 3) == round(float(G["auc"]), 3), (auc, float(G["auc"]))
+    lines = out1.splitlines()
+    k = next(i for i, ln in enumerate(lines) if ln.startswith("Confusion matrix"))
+    conf = [int(v) for v in re.findall(r"-?\d+", " ".join(lines[k + 1:k + 3]))]
+    assert conf == [int(v) for v in np.asarray(G["confusion"]).reshape(-1)], (conf, G["confusion"])

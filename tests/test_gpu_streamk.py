@@ -239,6 +239,9 @@ def test_stream_k_flags_reset_eager_and_graph():
         fwd(Yg, sp)
         ex = ctypes.c_void_p()
         ffi.check("end", L.jr_graph_end(sp, ctypes.byref(ex)))
+        # the capture's private flag region belongs to the graph exec and is
+        # released with it (captured regions were never freed)
+        assert L.jr_graph_regions(ex) == 1
         try:
             for _ in range(4):
                 Yg.zero_()
@@ -248,7 +251,61 @@ def test_stream_k_flags_reset_eager_and_graph():
                 assert torch.equal(Yg, ref)
         finally:
             ffi.check("destroy", L.jr_graph_destroy(ex))
+        assert L.jr_graph_regions(ex) == 0
         assert float(ref.abs().max()) > 0
     finally:
         ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, X8, 0, -1))
 
+
+
+@pytest.mark.parametrize("dtype,cfg", [(X8, SK0 + 11), (BF16, BF_SK0 + 0)])
+def test_stream_k_timeout_is_an_error_not_numbers(dtype, cfg):
+    """VERDICT r04 item 1b/1d, ADVICE r04: an owner block that gives up
+    waiting for a later piece's partial must not add the unpublished slot.
+    With the poll bound lowered to 0 (jr_debug_set_sk_spin_limit: every
+    owner gives up at once) the launch counts its failures into the device
+    error word and jr_device_check raises JR_ERR_DEVICE; the check resets the
+    hand-off flags the late publishers set, so the next launches on the same
+    stream (default bound) are bitwise the clean result again."""
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, cin, cout, kh, kw = 4, 8, 8, 2048, 384, 1, 1     # 30+ pieces per tile: every owner waits
+    d = ffi.ConvDesc(n, h, w, cin, cout, kh, kw, 1, 1, 0, 0, h, w, 0, cin, 0, cout)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    tdt = torch.bfloat16 if dtype == BF16 else torch.float32
+    X = torch.randn(n * h * w * cin, device="cuda", generator=g).to(tdt)
+    W = (torch.randn(kh * kw * cin * cout, device="cuda", generator=g) * 0.02).to(tdt)
+    ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, dtype, 0, cfg))
+    try:
+        wsb = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, dtype)
+        ws = torch.zeros(wsb // 4 + 4, device="cuda")
+        st = torch.zeros(2 * cout, device="cuda")
+
+        def fwd(Y):
+            ffi.check("fwd", L.jr_conv2d_fwd_bn_stats(ctypes.byref(d), dtype, X.data_ptr(), W.data_ptr(),
+                                                      Y.data_ptr(), 1e-3, st.data_ptr(), st.data_ptr() + 4 * cout,
+                                                      ws.data_ptr(), wsb, None))
+        ref = torch.zeros(n * h * w * cout, device="cuda", dtype=tdt)
+        fwd(ref)
+        torch.cuda.synchronize()
+        ffi.device_check()                        # a clean launch reports nothing
+        ffi.check("spin", L.jr_debug_set_sk_spin_limit(0))
+        try:
+            Y = torch.zeros_like(ref)
+            fwd(Y)
+            torch.cuda.synchronize()
+        finally:
+            ffi.check("spin", L.jr_debug_set_sk_spin_limit(1 << 22))
+        with pytest.raises(ffi.JRError) as ei:
+            ffi.device_check()
+        assert ei.value.status == ffi.JR_ERR_DEVICE and "stream-K" in str(ei.value)
+        ffi.device_check()                        # reported once, then clear
+        for _ in range(3):                        # the flags were reset: later launches are clean
+            Y = torch.zeros_like(ref)
+            fwd(Y)
+            torch.cuda.synchronize()
+            assert torch.equal(Y, ref)
+        ffi.device_check()
+        assert float(ref.float().abs().max()) > 0
+    finally:
+        ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, dtype, 0, -1))
