@@ -56,6 +56,8 @@ def parse():
                          "(TFRecord read + JPEG decode + every member's forward) over synthetic records")
     ap.add_argument("--members", type=int, default=10, help="ensemble mode: members resident on the GPU")
     ap.add_argument("--images", type=int, default=2048, help="ensemble mode: synthetic test images")
+    ap.add_argument("--ens-lanes", type=int, default=1,
+                    help="ensemble mode: branch lanes of the grouped EnsembleEngine (each with its own workspace)")
     ap.add_argument("--per-member", action="store_true",
                     help="ensemble mode: one engine per member instead of the grouped EnsembleEngine")
     ap.add_argument("--res", type=int, default=299)
@@ -244,12 +246,77 @@ def _write_records(out_dir: str, start: int, n: int, res: int, part: int) -> Non
     synth_records.write_split(out_dir, n, size=res, p=0.079, start=start, num_shards=1, name=f"test{part:02d}")
 
 
+def dist_setup(args):
+    """(rank, world, local, dist module or None): one process per GPU under
+    torch.distributed.run; backend nccl = RCCL.  Rehearsal knobs for the N>1
+    path on a one-GPU box (not for measurement): JR_BENCH_ONE_DEVICE=1 puts
+    every rank on cuda:0, JR_DIST_BACKEND=gloo replaces RCCL (which refuses
+    two ranks on one device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0 and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if os.environ.get("JR_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("JR_DIST_BACKEND", "nccl")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, local, dist
+
+
+def max_over_ranks(dist, v: float) -> float:
+    if not dist:
+        return v
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([v], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def grouped_conv_roofline(ens, steps: int = 3):
+    """The conv roofline of the grouped ensemble forward (BASELINE config 4):
+    HIP events (on the stream each call is enqueued on) bracket every grouped
+    conv + statistics launch of one lane-0 pass; algorithmic FLOPs = members x
+    batch x 2 x MACs per image."""
+    from jr import _ffi
+    calls, _ = ens._build_calls(ens.batch)
+    flops = sum(2 * n.macs_per_image() for n in ens.g.convs) * ens.batch * ens.members
+    pairs = []
+    for _ in range(steps):
+        for c in calls:
+            st = ens.lane_streams[c.lane]
+            if c.name == "conv_fwd":
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                rc = c.fn(*c.args)
+                e1.record(st)
+                pairs.append((e0, e1))
+            else:
+                rc = c.fn(*c.args)
+            if rc:
+                raise _ffi.JRError(c.name, rc, _ffi.last_error())
+    ens.synchronize()
+    t = sum(a.elapsed_time(b) for a, b in pairs) / 1e3 / steps
+    return flops, t, len(pairs) // steps
+
+
 def ensemble_bench(args) -> dict:
-    """BASELINE config 4 on one GPU: evaluate.predict_all (the -lm ensemble
-    loop of evaluate.py: records read and decoded once per batch on the host,
-    every resident member's forward on the GPU) timed end to end over
-    synthetic fundus TFRecords, next to its two halves alone: the input
-    pipeline (decode only) and the members' forwards on resident batches."""
+    """BASELINE config 4: evaluate.predict_all (the -lm ensemble loop of
+    evaluate.py: records read and decoded once per batch on the host, every
+    resident member's forward on the GPU) timed end to end over synthetic
+    fundus TFRecords, next to its two halves alone: the input pipeline
+    (decode only) and the members' forwards on resident batches.  Under
+    torch.distributed.run every rank takes the batches b = rank mod world in
+    dataset order (evaluate.py's sharding, no data-path collective); the time
+    is the max over ranks between two barriers, `value` = all images / it."""
     import multiprocessing as mp
     import shutil
     import tempfile
@@ -257,34 +324,47 @@ def ensemble_bench(args) -> dict:
     import evaluate
     import lib.dataset
     from jr.engine import Engine
+    rank, world, local, dist = dist_setup(args)
     B, res, n = args.batch or 32, args.res, args.images
-    d = tempfile.mkdtemp(prefix="jr_ensemble_")
+    d = None
     try:
-        parts = 8
-        per = -(-n // parts)
-        t0 = time.perf_counter()
-        with mp.get_context("spawn").Pool(parts) as pool:
-            pool.starmap(_write_records, [(d, k * per, min(per, n - k * per), res, k) for k in range(parts)
-                                          if n - k * per > 0])
-        log(f"{n} synthetic records in {time.perf_counter() - t0:.1f} s")
+        if rank == 0:            # one copy of the test set for every rank of the node
+            d = tempfile.mkdtemp(prefix="jr_ensemble_")
+            parts = 8
+            per = -(-n // parts)
+            t0 = time.perf_counter()
+            with mp.get_context("spawn").Pool(parts) as pool:
+                pool.starmap(_write_records, [(d, k * per, min(per, n - k * per), res, k) for k in range(parts)
+                                              if n - k * per > 0])
+            log(f"{n} synthetic records in {time.perf_counter() - t0:.1f} s")
+        if dist:
+            box = [d]
+            dist.broadcast_object_list(box, src=0)
+            d = box[0]
         math = args.conv_math if args.dtype == "f32" else "bf16"
         if args.per_member:
-            engines = [Engine(B, res, res, dtype=args.dtype, seed=m, train=False, conv_math=math, tiles=args.tiles)
-                       for m in range(args.members)]
+            engines = [Engine(B, res, res, device=local, dtype=args.dtype, seed=m, train=False, conv_math=math,
+                              tiles=args.tiles) for m in range(args.members)]
         else:                # every member's layer in one grouped launch (jr.ensemble)
             from jr.ensemble import EnsembleEngine
             from jr.inception import build_inception_v3
             from jr.init import init_params
             g = build_inception_v3(res, res)
-            engines = EnsembleEngine([init_params(g, m) for m in range(args.members)], B, res, res,
-                                     dtype=args.dtype, conv_math=math, tiles=args.tiles)
-        evaluate.predict_all(engines, d, B)          # warm-up pass (decoder threads, tiles, caches)
+            engines = EnsembleEngine([init_params(g, m) for m in range(args.members)], B, res, res, device=local,
+                                     dtype=args.dtype, conv_math=math, tiles=args.tiles, lanes=args.ens_lanes)
+        evaluate.predict_all(engines, d, B, rank, world)      # warm-up pass (decoder threads, tiles, caches)
+        if dist:
+            dist.barrier()
         t0 = time.perf_counter()
-        preds, labels, _ = evaluate.predict_all(engines, d, B)
-        t_all = time.perf_counter() - t0
-        assert preds[0].shape[0] == n and labels.shape[0] == n
+        preds, labels, ids = evaluate.predict_all(engines, d, B, rank, world)
+        t_mine = time.perf_counter() - t0
+        if dist:
+            dist.barrier()
+        t_all = max_over_ranks(dist, t_mine)
+        n_mine = labels.shape[0]
+        assert preds[0].shape[0] == n_mine and len(ids) == -(-n_mine // B)
         ds = lib.dataset.initialize_dataset(d, B, num_workers=evaluate.NUM_WORKERS, prefetch_buffer_size=2 * B,
-                                            image_dim=[res, res], decode_dtype="uint8")
+                                            image_dim=[res, res], decode_dtype="uint8", shard=(rank, world))
         t0 = time.perf_counter()
         it = iter(ds)
         batches = [b for b in it]
@@ -303,56 +383,57 @@ def ensemble_bench(args) -> dict:
         for e in group:
             e.synchronize()
         t_gpu = time.perf_counter() - t0
+        roof = None
+        if rank == 0 and not args.per_member and not args.no_roofline:
+            flops, tconv, nconv = grouped_conv_roofline(engines)
+            peak = PEAK_TFLOPS[math if math in ("x8", "x8p") else args.dtype]
+            ach = flops / tconv / 1e12
+            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(ach / peak, 4), "traffic": None,
+                    "kernel": f"grouped conv implicit-GEMM fwd + BN statistics, {args.members} members per launch "
+                              f"({nconv} launches/forward)",
+                    "conv_ms_per_forward": round(tconv * 1e3, 3),
+                    "algorithmic_gflop_per_forward": round(flops / 1e9, 1)}
+        if dist:
+            dist.barrier()
     finally:
-        shutil.rmtree(d, ignore_errors=True)
+        if rank == 0 and d:
+            shutil.rmtree(d, ignore_errors=True)
     M = args.members
-    return {
+    out = {
         "metric": f"ensemble eval images/sec, Inception-v3 {res}^2, {M} members, batch {B} (evaluate.py -lm)",
-        "value": round(n / t_all, 2), "unit": "images/sec", "n_gpus": 1, "steps": 1, "warmup": 1,
-        "ms_per_step": round(t_all / -(-n // B) * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "value": round(n / t_all, 2), "unit": "images/sec", "n_gpus": world, "steps": 1, "warmup": 1,
+        "ms_per_step": round(t_all / -(-n // (B * world)) * 1e3, 3), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": args.dtype,
         "data": f"{n} synthetic fundus-shaped JPEG q=100 TFRecords at {res}x{res} (jr.synth_records), random Keras "
                 f"init per member",
-        "config": {"workload": f"evaluate.predict_all: {M} resident members x {-(-n // B)} batches of {B}, each "
-                               f"batch read + decoded once (native JPEG, {evaluate.NUM_WORKERS} threads) and run "
-                               f"through every member ({'one engine per member' if args.per_member else 'every member in one grouped launch per layer'})",
-                   "model": "inception_v3", "global_batch": B, "seq_len": None,
-                   "parallelism": "dp1", "members": M, "tiles": group[0].tiles,
-                   "grouped": not args.per_member},
+        "config": {"workload": f"evaluate.predict_all: {M} resident members x {-(-n // B)} batches of {B} over "
+                               f"{world} rank(s) (batch b on rank b mod {world}), each batch read + decoded once "
+                               f"(native JPEG, {evaluate.NUM_WORKERS} threads per rank) and run through every member "
+                               f"({'one engine per member' if args.per_member else 'every member in one grouped launch per layer'})",
+                   "model": "inception_v3", "global_batch": B * world, "seq_len": None,
+                   "parallelism": f"dp{world} (batches sharded, no data-path collective)", "members": M,
+                   "tiles": group[0].tiles, "grouped": not args.per_member,
+                   "lanes": 1 if args.per_member else engines.nlanes},
         "member_images_per_s": round(n * M / t_all, 1),
-        "decode_only_images_per_s": round(n / t_dec, 1),
-        "gpu_forward_only_images_per_s": round(n / t_gpu, 1),
+        "decode_only_images_per_s": round(n_mine / t_dec, 1),
+        "gpu_forward_only_images_per_s": round(n_mine / t_gpu, 1),
         "bound": "decode" if t_dec > t_gpu else "gpu",
+        "roofline": roof,
     }
+    if dist:
+        dist.destroy_process_group()
+    return out if rank == 0 else None
 
 
 def main():
     args = parse()
     if args.mode == "ensemble":
         out = ensemble_bench(args)
-        print(json.dumps(out), flush=True)
+        if out is not None:
+            print(json.dumps(out), flush=True)
         return
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if rank == 0 and world > 1:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    # rehearsal knobs for the N>1 path on a one-GPU box (not for measurement):
-    # JR_BENCH_ONE_DEVICE=1 puts every rank on cuda:0, JR_DIST_BACKEND=gloo
-    # replaces RCCL (which refuses two ranks on one device)
-    if os.environ.get("JR_BENCH_ONE_DEVICE") == "1":
-        local = 0
-    backend = os.environ.get("JR_DIST_BACKEND", "nccl")
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+    rank, world, local, dist = dist_setup(args)
 
     from jr.engine import Engine
     from jr import synth
@@ -390,11 +471,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
     loss = eng.loss_value() if train else float(np.mean(eng.predictions()))
     if not np.isfinite(loss):
         raise SystemExit(f"non-finite {'loss' if train else 'prediction'} {loss}")
