@@ -149,6 +149,25 @@ int jr_conv2d_fwd_bn_stats_grouped(const jr_conv_desc* d, int dtype, int members
                                    int64_t x_member_stride, const void* w, int64_t w_member_stride, void* y,
                                    int64_t y_member_stride, float eps, float* mean, float* invstd,
                                    int64_t stats_member_stride, void* ws, size_t ws_bytes, void* stream);
+/* The statistics finalize folded into the BN apply (a kernel boundary fewer
+ * per conv2d_bn layer): jr_conv2d_bn_partials_layout says where the planned
+ * forward GEMM of this geometry leaves its BN-statistics partials in the
+ * workspace -- [2][N][P] fp32 (mean, M2) of R rows each (the last group the
+ * rest of the M rows) at ws + ws_offset -- and whether they are single-stage;
+ * jr_conv2d_fwd_bn_partials is jr_conv2d_fwd_bn_stats without the finalize
+ * (JR_ERR_UNSUPPORTED for two-stage partials); jr_bn_relu_apply_stats then
+ * combines the partials of its channels (bitwise the statistics
+ * jr_conv2d_fwd_bn_stats writes), applies BN + ReLU and writes mean / invstd
+ * for the backward.  The partials stay valid until the next call that uses
+ * the same workspace. */
+typedef struct jr_bn_partials {
+  int64_t ws_offset;
+  int32_t P, R, M, N;
+  int32_t single_stage;
+} jr_bn_partials;
+int jr_conv2d_bn_partials_layout(const jr_conv_desc* d, int dtype, jr_bn_partials* out);
+int jr_conv2d_fwd_bn_partials(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y, void* ws,
+                              size_t ws_bytes, void* stream);
 /* dx[.., x_c_off + ci] (+)= sum dy * w ; accumulate != 0 adds into dx */
 int jr_conv2d_bwd_data(const jr_conv_desc* d, int dtype, const void* dy, const void* w, void* dx,
                        int accumulate, void* ws, size_t ws_bytes, void* stream);
@@ -212,6 +231,15 @@ int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps, float
 int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,
                      const float* mean, const float* invstd, const float* beta, void* y, int32_t y_c_off,
                      int32_t y_c_stride, void* stream);
+/* jr_bn_relu_apply with the statistics finalize folded in: mean / invstd of
+ * the c channels come from the single-stage partials of the producing conv
+ * (jr_conv2d_fwd_bn_partials): part = ws + ws_offset, layout [2][n_total][P]
+ * of R rows each over m rows, this slice's channels starting at stat_c_off
+ * of n_total; mean / invstd [c] are written too (for the backward). */
+int jr_bn_relu_apply_stats(int dtype, const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,
+                           const float* part, int32_t P, int32_t R, int32_t n_total, int32_t stat_c_off, float eps,
+                           float* mean, float* invstd, const float* beta, void* y, int32_t y_c_off,
+                           int32_t y_c_stride, void* stream);
 /* jr_bn_relu_apply for the members of an ensemble in one launch: member i
  * reads x + i*x_member_stride, mean / invstd + i*stats_member_stride, beta +
  * i*beta_member_stride and writes y + i*y_member_stride (elements). */

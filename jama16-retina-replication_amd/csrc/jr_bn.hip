@@ -78,6 +78,29 @@ template <> struct Vec<uint16_t> {
   }
 };
 
+constexpr int kFoldCh = 256 / kStatsLanes;   // channels per folded apply block (32)
+// rows per folded apply block (JR_BN_FOLD_ROWS, read once; A/B knob): each
+// block re-combines its 32 channels' partials, so fewer rows per block means
+// more parallel blocks and more redundant partial reads
+static int fold_rows() {
+  static const int v = [] {
+    const char* e = std::getenv("JR_BN_FOLD_ROWS");
+    const int r = e ? std::atoi(e) : 0;
+    return r > 0 ? r : 256;
+  }();
+  return v;
+}
+// the backward's finalize folded into its apply: opt-in (JR_FOLD_BN_BWD=1,
+// read once) -- measured +0.14 ms/step bf16 against k_bn_finalize8 + apply
+// (profiles/r05_ab_rows_bf16.txt), same arithmetic either way
+static bool fold_bwd() {
+  static const bool on = [] {
+    const char* e = std::getenv("JR_FOLD_BN_BWD");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // Thread layout shared by every BN kernel: a row of c channels is tpr =
 // c / VW threads (one vector group q each); a 256-thread block covers rpp =
 // 256 / tpr rows per pass (row phase rr).  No index division in the loops.
@@ -374,6 +397,76 @@ __global__ void __launch_bounds__(256) k_bn_relu_apply(const T* __restrict__ x, 
   }
 }
 
+// k_bn_relu_apply with the statistics finalize folded in: block (bx, by)
+// first combines the conv's single-stage partials of the 32 channels of group
+// by (stats_combine8: 8 lanes per channel, bitwise what k_stats_finalize8
+// writes) into LDS -- blocks with bx == 0 also store them as the layer's
+// mean / invstd -- then applies BN + ReLU to rows [bx*rpb, (bx+1)*rpb) of
+// those channels, thread (q, rr) one 16-byte vector q of the group and rows
+// rr, rr + rpp, ... (the arithmetic of k_bn_relu_apply).
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_relu_apply_stats(const T* __restrict__ x, int xs, int64_t m, int c,
+                                                             const float* __restrict__ pm, const float* __restrict__ pq,
+                                                             int P, int R, float eps, float* mean_out,
+                                                             float* invstd_out, const float* __restrict__ beta, T* y,
+                                                             int y_off, int y_stride, int rpb) {
+  constexpr int VW = Vec<T>::N;
+  __shared__ float s_mu[kFoldCh], s_is[kFoldCh];
+  const int t = threadIdx.x;
+  const int c0 = blockIdx.y * kFoldCh;
+  const int cg = min(kFoldCh, c - c0);
+  {
+    const int slot = t / kStatsLanes, j = t % kStatsLanes;
+    if (slot < cg) {
+      const int ch = c0 + slot;
+      float mu, is;
+      stats_combine8(pm + (int64_t)ch * P, pq + (int64_t)ch * P, P, R, (int)m, eps, j, &mu, &is);
+      if (j == 0) {
+        s_mu[slot] = mu;
+        s_is[slot] = is;
+        if (blockIdx.x == 0) {
+          mean_out[ch] = mu;
+          invstd_out[ch] = is;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int tpr = cg / VW;
+  const int rpp = 256 / tpr;
+  const int q = t % tpr, rr = t / tpr;
+  if (rr >= rpp) return;
+  float mu[VW], is[VW], be[VW];
+#pragma unroll
+  for (int k = 0; k < VW; ++k) {
+    mu[k] = s_mu[q * VW + k]; is[k] = s_is[q * VW + k]; be[k] = beta[c0 + q * VW + k];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(m, r0 + rpb);
+  const int co = c0 + q * VW;
+  for (int64_t rb = r0 + rr; rb < r1; rb += (int64_t)rpp * kAppUnroll) {
+    // unconditional loads (rows past the block re-read its last row), unpacked
+    // after all were issued (as in k_bn_relu_apply)
+    uint4 xr[kAppUnroll];
+#pragma unroll
+    for (int u = 0; u < kAppUnroll; ++u) {
+      const int64_t r = min(rb + (int64_t)u * rpp, r1 - 1);
+      xr[u] = *reinterpret_cast<const uint4*>(x + r * xs + co);
+    }
+#pragma unroll
+    for (int u = 0; u < kAppUnroll; ++u) pin(xr[u]);
+#pragma unroll
+    for (int u = 0; u < kAppUnroll; ++u) {
+      const int64_t r = rb + (int64_t)u * rpp;
+      if (r >= r1) break;
+      float xv[VW], o[VW];
+      Vec<T>::unpack(xr[u], xv);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) o[k] = fmaxf(bn_pre(xv[k], mu[k], is[k], be[k]), 0.f);
+      Vec<T>::st(y + r * y_stride + y_off + co, o);
+    }
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(BnSegs sg, const T* __restrict__ x, int xs, int64_t m,
                                                            int c, const float* __restrict__ mean,
@@ -425,6 +518,134 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(BnSegs sg, const T* _
       o[j] = is[j] * (g - c1[j] - xh * c2[j]);
     }
     Vec<T>::st(dx + r * xs + q * VW, o);
+  }
+}
+
+// Canonical combine of ONE channel's backward-reduce partials when there are
+// at most kFoldMaxP of them (fp64 (sum dy', sum dy' xhat) per chunk): an
+// aligned group of 8 lanes, lane j summing chunks j, j+8, ... in order, then
+// an xor butterfly.  k_bn_finalize8 and k_bn_relu_bwd_apply_fold share it, so
+// the folded backward is bitwise the three-launch one.
+__device__ __forceinline__ void bwd_combine8(const double* __restrict__ p0, const double* __restrict__ p1, int nch,
+                                             int j, double* s0, double* s1) {
+  double a = 0, b = 0;
+  constexpr int U = 8;
+  for (int i0 = j; i0 < nch; i0 += kStatsLanes * U) {
+    double va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ic = min(i0 + kStatsLanes * u, nch - 1);
+      va[u] = p0[ic];
+      vb[u] = p1[ic];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + kStatsLanes * u < nch) {
+        a += va[u];
+        b += vb[u];
+      }
+  }
+#pragma unroll
+  for (int o = kStatsLanes / 2; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, kStatsLanes);
+    b += __shfl_xor(b, o, kStatsLanes);
+  }
+  *s0 = a;
+  *s1 = b;
+}
+
+// k_bn_finalize<1> for at most kFoldMaxP chunks: 32 channels per block.
+__global__ void __launch_bounds__(256) k_bn_finalize8(const double* __restrict__ part, int nchunks, int c, int64_t m,
+                                                      float* k1, float* k2, BnSegs sg) {
+  const int k = blockIdx.x * (256 / kStatsLanes) + threadIdx.x / kStatsLanes, j = threadIdx.x % kStatsLanes;
+  if (k >= c) return;   // (whole 8-lane groups)
+  double s0, s1;
+  bwd_combine8(part + (int64_t)k * nchunks, part + (int64_t)(c + k) * nchunks, nchunks, j, &s0, &s1);
+  if (j != 0) return;
+  const double inv_m = 1.0 / (double)m;
+  k1[k] = (float)(s0 * inv_m);
+  k2[k] = (float)(s1 * inv_m);
+  const int sgi = seg_of(sg, k);
+  sg.dbeta[sgi][k - sg.c0[sgi]] = (float)s0;
+}
+
+// The backward's finalize folded into its apply: block (bx, by) combines the
+// reduce's partials of the 32 channels of group by (bwd_combine8; bx == 0
+// also stores dbeta), then applies the backward to rows [bx*rpb, (bx+1)*rpb)
+// of those channels with the arithmetic of k_bn_relu_bwd_apply.
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_relu_bwd_apply_fold(BnSegs sg, const T* __restrict__ x, int xs, int64_t m,
+                                                                int c, const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd,
+                                                                const double* __restrict__ part, int nchunks, T* dx,
+                                                                int rpb) {
+  constexpr int VW = Vec<T>::N;
+  __shared__ float s_k1[kFoldCh], s_k2[kFoldCh];
+  const int t = threadIdx.x;
+  const int c0 = blockIdx.y * kFoldCh;
+  const int cg = min(kFoldCh, c - c0);
+  {
+    const int slot = t / kStatsLanes, j = t % kStatsLanes;
+    if (slot < cg) {
+      const int k = c0 + slot;
+      double s0, s1;
+      bwd_combine8(part + (int64_t)k * nchunks, part + (int64_t)(c + k) * nchunks, nchunks, j, &s0, &s1);
+      if (j == 0) {
+        const double inv_m = 1.0 / (double)m;
+        s_k1[slot] = (float)(s0 * inv_m);
+        s_k2[slot] = (float)(s1 * inv_m);
+        if (blockIdx.x == 0) {
+          const int sgi = seg_of(sg, k);
+          sg.dbeta[sgi][k - sg.c0[sgi]] = (float)s0;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int tpr = cg / VW;
+  const int rpp = 256 / tpr;
+  const int q = t % tpr, rr = t / tpr;
+  if (rr >= rpp) return;
+  const int ch = c0 + q * VW;
+  const int sgi = seg_of(sg, ch), lc = ch - sg.c0[sgi];
+  const T* dy = static_cast<const T*>(sg.dy[sgi]) + sg.dy_off[sgi] + lc;
+  const int dy_stride = sg.dy_stride[sgi];
+  float mu[VW], is[VW], be[VW], c1[VW], c2[VW];
+#pragma unroll
+  for (int k = 0; k < VW; ++k) {
+    mu[k] = mean[ch + k]; is[k] = invstd[ch + k]; be[k] = sg.beta[sgi][lc + k];
+    c1[k] = s_k1[q * VW + k]; c2[k] = s_k2[q * VW + k];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(m, r0 + rpb);
+  for (int64_t rb = r0 + rr; rb < r1; rb += (int64_t)rpp * kAppUnroll) {
+    uint4 xr[kAppUnroll], gr[kAppUnroll];
+#pragma unroll
+    for (int u = 0; u < kAppUnroll; ++u) {
+      const int64_t r = min(rb + (int64_t)u * rpp, r1 - 1);
+      xr[u] = *reinterpret_cast<const uint4*>(x + r * xs + ch);
+      gr[u] = *reinterpret_cast<const uint4*>(dy + r * dy_stride);
+    }
+#pragma unroll
+    for (int u = 0; u < kAppUnroll; ++u) {
+      pin(xr[u]);
+      pin(gr[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kAppUnroll; ++u) {
+      const int64_t r = rb + (int64_t)u * rpp;
+      if (r >= r1) break;
+      float xv[VW], gv[VW], o[VW];
+      Vec<T>::unpack(xr[u], xv);
+      Vec<T>::unpack(gr[u], gv);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) {
+        const float xh = bn_xhat(xv[k], mu[k], is[k]);
+        const float pre = __fadd_rn(xh, be[k]);
+        const float g = pre > 0.f ? gv[k] : 0.f;
+        o[k] = is[k] * (g - c1[k] - xh * c2[k]);
+      }
+      Vec<T>::st(dx + r * xs + ch, o);
+    }
   }
 }
 
@@ -514,6 +735,38 @@ JR_API int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x
                          as_stream(stream));
 }
 
+JR_API int jr_bn_relu_apply_stats(int dtype, const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,
+                                  const float* part, int32_t P, int32_t R, int32_t n_total, int32_t stat_c_off,
+                                  float eps, float* mean, float* invstd, const float* beta, void* y, int32_t y_c_off,
+                                  int32_t y_c_stride, void* stream) {
+  int rc = check_common(dtype, m, c);
+  if (rc) return rc;
+  if (!x || !part || !mean || !invstd || !beta || !y) return fail(JR_ERR_INVALID, "bn_relu_apply_stats: null pointer");
+  if (!check_slice(dtype, x_c_off, x_c_stride, c) || !check_slice(dtype, y_c_off, y_c_stride, c))
+    return fail(JR_ERR_INVALID, "bn_relu_apply_stats: bad input / output slice");
+  if (P < 1 || R < 1 || (int64_t)P * R < m || stat_c_off < 0 || stat_c_off + c > n_total || m >= (1LL << 31))
+    return fail(JR_ERR_INVALID, "bn_relu_apply_stats: partials inconsistent with the slice");
+  const size_t esz = dtype == JR_BF16 ? 2 : 4;
+  x = static_cast<const char*>(x) + (size_t)x_c_off * esz;
+  const float* pm = part + (int64_t)stat_c_off * P;
+  const float* pq = part + (int64_t)(n_total + stat_c_off) * P;
+  // rows per block: a multiple of one pass x unroll (the 32-channel group's
+  // widest pass), about JR_BN_FOLD_ROWS (each block re-combines its group's
+  // partials: fewer, longer blocks read them fewer times)
+  const int vw = vec_width(dtype);
+  const int step = 256 / (kFoldCh / vw) * kAppUnroll;
+  const int rpb = (int)std::max<int64_t>(step, (int64_t)(fold_rows() + step - 1) / step * step);
+  const dim3 grid((unsigned)ceil_div(m, rpb), (unsigned)ceil_div(c, kFoldCh));
+  hipStream_t s = as_stream(stream);
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_bn_relu_apply_stats<float>, grid, dim3(256), 0, s, (const float*)x, x_c_stride, m, c, pm, pq,
+                       P, R, eps, mean, invstd, beta, (float*)y, y_c_off, y_c_stride, rpb);
+  else
+    hipLaunchKernelGGL(k_bn_relu_apply_stats<uint16_t>, grid, dim3(256), 0, s, (const uint16_t*)x, x_c_stride, m, c,
+                       pm, pq, P, R, eps, mean, invstd, beta, (uint16_t*)y, y_c_off, y_c_stride, rpb);
+  return check_launch("bn_relu_apply_stats");
+}
+
 JR_API int jr_bn_relu_apply_grouped(int dtype, int32_t members, const void* x, int32_t x_c_off, int32_t x_c_stride,
                                     int64_t x_member_stride, int64_t m, int32_t c, const float* mean,
                                     const float* invstd, int64_t stats_member_stride, const float* beta,
@@ -568,8 +821,26 @@ static int bn_bwd_launch(int dtype, const BnSegs& sg, const void* x, int32_t x_c
                        x_c_stride, sg, m, c, g.rows_per_chunk, mean, invstd, part);
   int rc = check_launch("bn_bwd reduce");
   if (rc) return rc;
-  hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, g.nchunks, c, m, 0.f,
-                     k1, k2, sg);
+  if (g.nchunks <= kFoldMaxP) {
+    if (fold_bwd()) {   // the finalize inside the apply: one kernel boundary fewer
+      const int vw = vec_width(dtype);
+      const int step = 256 / (kFoldCh / vw) * kAppUnroll;
+      const int rpb = (int)std::max<int64_t>(step, (int64_t)(fold_rows() + step - 1) / step * step);
+      const dim3 grid((unsigned)ceil_div(m, rpb), (unsigned)ceil_div(c, kFoldCh));
+      if (dtype == JR_F32)
+        hipLaunchKernelGGL(k_bn_relu_bwd_apply_fold<float>, grid, dim3(256), 0, s, sg, (const float*)x, x_c_stride, m,
+                           c, mean, invstd, (const double*)part, g.nchunks, (float*)dx, rpb);
+      else
+        hipLaunchKernelGGL(k_bn_relu_bwd_apply_fold<uint16_t>, grid, dim3(256), 0, s, sg, (const uint16_t*)x,
+                           x_c_stride, m, c, mean, invstd, (const double*)part, g.nchunks, (uint16_t*)dx, rpb);
+      return check_launch("bn_bwd apply (fold)");
+    }
+    hipLaunchKernelGGL(k_bn_finalize8, dim3((int)ceil_div(c, kFoldCh)), dim3(256), 0, s, (const double*)part,
+                       g.nchunks, c, m, k1, k2, sg);
+  } else {
+    hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, g.nchunks, c, m, 0.f,
+                       k1, k2, sg);
+  }
   rc = check_launch("bn_bwd finalize");
   if (rc) return rc;
   return bn_bwd_apply_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, k1, k2, dx, s);

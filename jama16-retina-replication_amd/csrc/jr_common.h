@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <cstdlib>
 #include <string>
 
 #include "jr_error.h"
@@ -58,6 +59,53 @@ __device__ __forceinline__ float bn_xhat(float x, float mean, float invstd) {
 }
 __device__ __forceinline__ float bn_pre(float x, float mean, float invstd, float beta) {
   return __fadd_rn(bn_xhat(x, mean, invstd), beta);
+}
+
+// Canonical combine of ONE channel's fused BN-statistics partials (the conv
+// epilogue's / split-K reduce's per-row-group (mean, M2) of R rows each; the
+// last group holds the rest of the M rows) into (mean, invstd): an aligned
+// group of 8 lanes, lane j summing partials j, j+8, ... in order, shifted by
+// the first partial's mean K, in fp64; an xor butterfly over the 8 lanes.
+// k_stats_finalize8 (jr_conv.hip) and jr_bn_relu_apply_stats (jr_bn.hip, the
+// finalize folded into the BN apply) both call this, so they give bitwise the
+// same statistics.  Every lane of the group returns the result.
+constexpr int kStatsLanes = 8;
+constexpr int kFoldMaxP = 512;   // partials per channel that this combine (and so the fold) takes
+__device__ __forceinline__ void stats_combine8(const float* __restrict__ pm, const float* __restrict__ pq, int P,
+                                               int R, int M, float eps, int j, float* mean, float* invstd) {
+  const double K = pm[0];
+  double sn = 0, sd = 0, sq = 0;
+  constexpr int U = 16;   // loads in flight per lane and array
+  for (int i0 = j; i0 < P; i0 += kStatsLanes * U) {
+    float vm[U], vq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {   // clamped unconditional loads, all issued before any use
+      const int ic = min(i0 + kStatsLanes * u, P - 1);
+      vm[u] = pm[ic];
+      vq[u] = pq[ic];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + kStatsLanes * u;
+      if (i < P) {
+        const double c = (double)min(max(M - i * R, 0), R);
+        const double d = (double)vm[u] - K;
+        sn += c;
+        sd += c * d;
+        sq += (double)vq[u] + c * d * d;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = kStatsLanes / 2; o > 0; o >>= 1) {
+    sn += __shfl_xor(sn, o, kStatsLanes);
+    sd += __shfl_xor(sd, o, kStatsLanes);
+    sq += __shfl_xor(sq, o, kStatsLanes);
+  }
+  const double dm = sn > 0 ? sd / sn : 0.0;
+  const double m2 = fmax(sq - sn * dm * dm, 0.0);
+  *mean = (float)(K + dm);
+  *invstd = (float)(1.0 / sqrt(m2 / (double)M + (double)eps));
 }
 
 // Element load/store of an activation in the path dtype.

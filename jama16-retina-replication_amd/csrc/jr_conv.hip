@@ -922,6 +922,7 @@ struct StatsReq {
   float eps;
   float* mean;
   float* invstd;
+  bool defer = false;   // leave the single-stage partials in ws for jr_bn_relu_apply_stats
 };
 
 static void stats_geom(int dtype, const Plan& p, int* P, int* R) {
@@ -1049,6 +1050,60 @@ static size_t member_ws(int dtype, const Plan& p, bool stats) {
   return align256(stats ? align256(plan_ws(p)) + stats_ws(dtype, p) : plan_ws(p));
 }
 
+// (mean, invstd) from the statistics partials [2][N][P] of R rows each
+// (member stride pm bytes): P <= kFoldMaxP -- k_stats_finalize8, the
+// arithmetic jr_bn_relu_apply_stats shares (st->defer: left to it); P <=
+// kStatsChunk -- one 256-thread combine per channel; else two stages.
+static int finalize_stats(float* stats, int sP, int sR, int M, int N, int members, long long pm, const StatsReq* st,
+                          long long st_mb, hipStream_t s) {
+  if (sP <= kFoldMaxP) {
+    if (st->defer) return JR_OK;          // the BN apply combines them (jr_bn_relu_apply_stats)
+    hipLaunchKernelGGL(k_stats_finalize8, dim3((int)ceil_div(N, 256 / kStatsLanes), 1, members), dim3(256), 0, s,
+                       (const float*)stats, sP, sR, M, N, st->eps, st->mean, st->invstd, pm, st_mb);
+  } else if (st->defer) {
+    return fail(JR_ERR_UNSUPPORTED, "conv fwd partials: more than kFoldMaxP statistics partials cannot be deferred");
+  } else if (sP <= kStatsChunk) {
+    hipLaunchKernelGGL(k_stats_finalize, dim3(N, 1, members), dim3(256), 0, s, (const float*)stats,
+                       (const float*)nullptr, sP, sR, M, N, sP, st->eps, st->mean, st->invstd, (float*)nullptr, pm,
+                       st_mb);
+  } else {   // two stages: per-chunk (mean, M2, n), then the final combine
+    const int S = (int)ceil_div(sP, kStatsChunk);
+    float* s2 = stats + 2 * (size_t)N * sP;
+    hipLaunchKernelGGL(k_stats_finalize, dim3(N, S, members), dim3(256), 0, s, (const float*)stats,
+                       (const float*)nullptr, sP, sR, M, N, kStatsChunk, st->eps, (float*)nullptr, (float*)nullptr, s2,
+                       pm, st_mb);
+    const int rc = check_launch("conv stats combine");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_stats_finalize, dim3(N, 1, members), dim3(256), 0, s, (const float*)s2,
+                       (const float*)(s2 + 2 * (size_t)N * S), S, 0, M, N, S, st->eps, st->mean, st->invstd,
+                       (float*)nullptr, pm, st_mb);
+  }
+  return check_launch("conv stats finalize");
+}
+
+// conv2d_1 as the direct kernel (jr_conv_direct.hip), its statistics
+// partials at ws (member m at ws + m * wsm) and finalized as any GEMM's.
+static size_t conv1_direct_ws(const jr_conv_desc* d) {
+  int P, R;
+  conv1_direct_partials(d, &P, &R);
+  return align256((size_t)2 * d->c_out * P * sizeof(float));
+}
+
+static int run_conv1_direct(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y, void* ws,
+                            size_t ws_bytes, hipStream_t s, const StatsReq* st, int members = 1, long long x_mb = 0,
+                            long long w_mb = 0, long long y_mb = 0, long long st_mb = 0) {
+  int P, R;
+  conv1_direct_partials(d, &P, &R);
+  const size_t wsm = conv1_direct_ws(d);
+  if (st && (!ws || ws_bytes < wsm * members)) return fail(JR_ERR_WORKSPACE, "conv1 direct: workspace too small");
+  float* stats = st ? static_cast<float*>(ws) : nullptr;
+  launch_conv1_direct(d, dtype, x, w, y, stats, members, x_mb, w_mb, y_mb, (long long)wsm, s);
+  int rc = check_launch("conv1 direct");
+  if (rc || !st) return rc;
+  const long long M = (long long)d->n * d->ho * d->wo;
+  return finalize_stats(stats, P, R, (int)M, d->c_out, members, (long long)wsm, st, st_mb, s);
+}
+
 template <int OP>
 static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, size_t ws_bytes, hipStream_t s,
                     const StatsReq* st = nullptr, bool defer = false, int members = 1, long long st_mb = 0) {
@@ -1150,24 +1205,7 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
       rc = check_launch("conv split-k reduce + stats");
       if (rc) return rc;
     }
-    const long long pm = (long long)wsm;   // partials' member stride
-    if (sP <= kStatsChunk) {
-      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N, 1, members), dim3(256), 0, s, (const float*)a.stats,
-                         (const float*)nullptr, sP, sR, p.M, p.N, sP, st->eps, st->mean, st->invstd, (float*)nullptr,
-                         pm, st_mb);
-    } else {   // two stages: per-chunk (mean, M2, n), then the final combine
-      const int S = (int)ceil_div(sP, kStatsChunk);
-      float* s2 = a.stats + 2 * (size_t)p.N * sP;
-      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N, S, members), dim3(256), 0, s, (const float*)a.stats,
-                         (const float*)nullptr, sP, sR, p.M, p.N, kStatsChunk, st->eps, (float*)nullptr,
-                         (float*)nullptr, s2, pm, st_mb);
-      rc = check_launch("conv stats combine");
-      if (rc) return rc;
-      hipLaunchKernelGGL(k_stats_finalize, dim3(p.N, 1, members), dim3(256), 0, s, (const float*)s2,
-                         (const float*)(s2 + 2 * (size_t)p.N * S), S, 0, p.M, p.N, S, st->eps, st->mean, st->invstd,
-                         (float*)nullptr, pm, st_mb);
-    }
-    return check_launch("conv stats finalize");
+    return finalize_stats(a.stats, sP, sR, p.M, p.N, members, (long long)wsm, st, st_mb, s);
   }
   if (members > 1) return fail(JR_ERR_UNSUPPORTED, "conv grouped: forward with BN statistics only");
   if (p.splits <= 1 || defer) return rc;
@@ -1217,7 +1255,8 @@ static size_t ws_bytes_for(const jr_conv_desc* d, int op, int dtype) {
     }
   }
   // 2x: room for the autotuner's doubled split-K factors; FWD: the statistics
-  // partials live behind the slabs
+  // partials live behind the slabs (or, conv2d_1's direct kernel, at 0)
+  if (op == OP_FWD && conv1_direct_ok(d, dtype)) sw = std::max(sw, conv1_direct_ws(d));
   return op == OP_FWD ? align256(2 * w) + sw : 2 * w;
 }
 
@@ -1260,6 +1299,7 @@ static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, con
   hipStream_t s = as_stream(stream);
   void* out = C;
   if (op == OP_FWD) {
+    if (force_cfg < 0 && conv1_direct_ok(d, dtype)) return run_conv1_direct(d, dtype, A, B, C, ws, ws_bytes, s, st);
     a.c_off = d->y_c_off; a.c_stride = d->y_c_stride;
     return run_gemm<OP_FWD>(dtype, a, plan_for(d, op, dtype, nullptr, force_cfg), out, ws, ws_bytes, s, st);
   }
@@ -1375,6 +1415,27 @@ static int autotune(const jr_conv_desc* d, int op, int dtype, const void* A, con
 // the first stage of a two-stage combine).  Block (n, s) combines partials
 // [s*chunk, (s+1)*chunk) of channel n; with gridDim.y == 1 it finalizes
 // (mean, invstd), else it writes one (mean, M2, count) partial per chunk.
+// Single-stage statistics finalize: 32 channels per block, 8 lanes each
+// (stats_combine8, jr_common.h: the arithmetic jr_bn_relu_apply_stats shares).
+__global__ void __launch_bounds__(256) k_stats_finalize8(const float* __restrict__ part, int P, int R, int M, int N,
+                                                         float eps, float* mean, float* invstd, long long p_mb,
+                                                         long long st_mb) {
+  if (gridDim.z > 1) {   // grouped: member blockIdx.z
+    const long long mz = blockIdx.z;
+    part = reinterpret_cast<const float*>(reinterpret_cast<const char*>(part) + mz * p_mb);
+    mean = reinterpret_cast<float*>(reinterpret_cast<char*>(mean) + mz * st_mb);
+    invstd = reinterpret_cast<float*>(reinterpret_cast<char*>(invstd) + mz * st_mb);
+  }
+  const int n = blockIdx.x * (256 / kStatsLanes) + threadIdx.x / kStatsLanes, j = threadIdx.x % kStatsLanes;
+  if (n >= N) return;   // (whole 8-lane groups)
+  float mu, is;
+  stats_combine8(part + (long long)n * P, part + (long long)(N + n) * P, P, R, M, eps, j, &mu, &is);
+  if (j == 0) {
+    mean[n] = mu;
+    invstd[n] = is;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict__ part, const float* __restrict__ cnt,
                                                         int P, int R, int M, int N, int chunk, float eps,
                                                         float* mean, float* invstd, float* out, long long p_mb,
@@ -1549,6 +1610,44 @@ JR_API int jr_conv2d_fwd_bn_stats(const jr_conv_desc* d, int dtype, const void* 
   return run_conv(d, OP_FWD, dtype, x, w, y, 0, ws, ws_bytes, stream, -1, -1, &st);
 }
 
+// Where the planned forward GEMM leaves its BN-statistics partials in the
+// workspace ([2][N][P] fp32 (mean, M2) of R rows each, at ws + ws_offset),
+// and whether they are single-stage (P <= kStatsChunk: then
+// jr_conv2d_fwd_bn_partials + jr_bn_relu_apply_stats may replace
+// jr_conv2d_fwd_bn_stats + jr_bn_relu_apply).  The plan is the one the next
+// call of this geometry would use (pinned / tuned / planner).
+JR_API int jr_conv2d_bn_partials_layout(const jr_conv_desc* d, int dtype, jr_bn_partials* out) {
+  int rc = validate(d, OP_FWD, dtype);
+  if (rc) return rc;
+  if (!out) return fail(JR_ERR_INVALID, "bn_partials_layout: null output");
+  int P = 0, R = 0;
+  if (conv1_direct_ok(d, dtype)) {
+    conv1_direct_partials(d, &P, &R);
+    out->ws_offset = 0;
+  } else {
+    const Plan p = plan_for(d, OP_FWD, dtype, nullptr);
+    stats_geom(dtype, p, &P, &R);
+    out->ws_offset = (int64_t)align256(plan_ws(p));
+  }
+  out->P = P;
+  out->R = R;
+  out->M = d->n * d->ho * d->wo;
+  out->N = d->c_out;
+  out->single_stage = P <= kFoldMaxP ? 1 : 0;
+  return JR_OK;
+}
+
+// jr_conv2d_fwd_bn_stats without the statistics finalize: the GEMM (and its
+// split-K reduce) write y and the single-stage partials into ws
+// (jr_conv2d_bn_partials_layout); jr_bn_relu_apply_stats combines them.
+JR_API int jr_conv2d_fwd_bn_partials(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y,
+                                     void* ws, size_t ws_bytes, void* stream) {
+  float dummy = 0.f;   // (never written: the finalize is skipped)
+  StatsReq st{0.f, &dummy, &dummy};
+  st.defer = true;
+  return run_conv(d, OP_FWD, dtype, x, w, y, 0, ws, ws_bytes, stream, -1, -1, &st);
+}
+
 // Grouped forward (ensemble members): the same conv geometry for `members`
 // models in ONE launch per GEMM (blockIdx.y = member), each member with its
 // own input, filter, output and BN statistics at the given element strides;
@@ -1574,6 +1673,12 @@ JR_API int jr_conv2d_fwd_bn_stats_grouped(const jr_conv_desc* d, int dtype, int 
       ((x_member_stride * esz) | (w_member_stride * esz) | (y_member_stride * esz)) & 15 ||
       x_member_stride < 0 || w_member_stride < 0 || y_member_stride < 0 || stats_member_stride < 0)
     return fail(JR_ERR_INVALID, "conv grouped: tensors and member strides must be 16-byte aligned, strides >= 0");
+  if (conv1_direct_ok(d, dtype)) {   // every member's conv2d_1 in one direct launch (bitwise the single call)
+    const StatsReq st{eps, mean, invstd};
+    const long long wsz = dtype == JR_BF16 ? 2 : 4;
+    return run_conv1_direct(d, dtype, x, w, y, ws, ws_bytes, as_stream(stream), &st, members, x_member_stride * esz,
+                            w_member_stride * wsz, y_member_stride * esz, stats_member_stride * 4);
+  }
   ConvArgs a{};
   fill_common(a, d, dtype);
   a.A = static_cast<const float*>(x);

@@ -1,0 +1,220 @@
+// jr_conv_direct.hip — the image layer conv2d_1 (c_in 3 stored 4 fp32 / 8
+// bf16 wide, 3x3 stride 2 'valid', c_out 32; train.py:129-130 -> Keras
+// conv2d_bn) as a direct VALU convolution with the fused BN statistics.
+//
+// As an implicit GEMM this layer is memory-bound (K = 27: 2.46 GFLOP per
+// B=64 step against 91.5 MB of fp32 image in and 182 MB of output) and ran
+// at 18-27 TF/s (`profiles/r04a_*_step_breakdown.txt`): the 16-deep K-tiles
+// padded 27 to 36 or 48 and the epilogue wrote 128 x 32 tiles.  Here a
+// thread owns 8 output channels of one pixel (4 threads per pixel, so a
+// wave's stores are 2 KB contiguous: 16 pixels x 32 channels), keeps its 72
+// weights' worth of taps in LDS (fp32, [tap][ci][co], from the fp32 HWIO
+// master or the bf16 W^T copy), and accumulates the 27 products of each
+// output in fp32 FMA in (r, c, ci) order -- every product is exact in fp32
+// for bf16 operands and fp32-rounded once for fp32 ones, as in the fp32 MFMA
+// kernel.  The block (256 threads) covers R = 1024 consecutive output
+// pixels: 16 rounds of 16 pixels per wave; per channel each thread keeps
+// shifted sums over its 16 pixels, the 16 lanes of a channel group combine
+// by a fixed Chan butterfly, the 4 waves in wave order through LDS, and the
+// block writes one (mean, M2) partial per channel: stats[2][32][P], P =
+// ceil(M / 1024) -- one finalize stage at every BASELINE size (1,388 at 299^2 B=64).
+#include "jr_conv_impl.h"
+
+namespace jr {
+
+constexpr int kD1Rows = 1024;   // output pixels per block (= R of the statistics partials)
+constexpr int kD1Cout = 32;
+
+// Chan combine of (n, mean, M2) partials, fp32 (k_splitk_reduce_stats' form).
+__device__ __forceinline__ void chan_combine(float& na, float& ma, float& qa, float nb, float mb, float qb) {
+  const float nn = na + nb;
+  if (nb > 0.f) {
+    const float fa = na / nn, fb = nb / nn, w = na * nb / nn, d = mb - ma;
+    ma = ma * fa + mb * fb;
+    qa = qa + qb + d * d * w;
+    na = nn;
+  }
+}
+
+// TW = weight element type as passed (float: HWIO [3][3][cin][32]; uint16_t:
+// the bf16 W^T copy [32][3][3][c8]); TX / TY = activation element types.
+template <typename TX, typename TW>
+__global__ void __launch_bounds__(256) k_conv1_direct(const TX* __restrict__ x, int xs, const TW* __restrict__ wt,
+                                                      TX* __restrict__ y, int n, int h, int w, int ho, int wo,
+                                                      int cin, int c8, float* __restrict__ stats, int P,
+                                                      long long x_mb, long long w_mb, long long y_mb, long long s_mb) {
+  constexpr bool BF = sizeof(TX) == 2;
+  if (gridDim.y > 1) {   // grouped ensemble members (blockIdx.y): byte strides
+    const long long mb = blockIdx.y;
+    x = reinterpret_cast<const TX*>(reinterpret_cast<const char*>(x) + mb * x_mb);
+    wt = reinterpret_cast<const TW*>(reinterpret_cast<const char*>(wt) + mb * w_mb);
+    y = reinterpret_cast<TX*>(reinterpret_cast<char*>(y) + mb * y_mb);
+    if (stats) stats = reinterpret_cast<float*>(reinterpret_cast<char*>(stats) + mb * s_mb);
+  }
+  __shared__ float s_w[9 * 4 * kD1Cout];          // [tap][ci][co], ci < 4
+  __shared__ float s_red[3][4][kD1Cout];          // per wave: (n, mean, M2) per channel
+  const int t = threadIdx.x;
+  for (int i = t; i < 9 * 4 * kD1Cout; i += 256) {
+    const int co = i % kD1Cout, ci = (i / kD1Cout) % 4, tap = i / (4 * kD1Cout);
+    float v = 0.f;
+    if (ci < cin) {
+      if constexpr (sizeof(TW) == 2)
+        v = bf2f(reinterpret_cast<const uint16_t*>(wt)[(long long)co * 9 * c8 + tap * c8 + ci]);
+      else
+        v = reinterpret_cast<const float*>(wt)[((long long)tap * cin + ci) * kD1Cout + co];
+    }
+    s_w[i] = v;
+  }
+  __syncthreads();
+  const int lane = t & 63, wave = t >> 6;
+  const int g = lane & 3;                 // channel group: channels 8g .. 8g+7
+  const int pl = lane >> 2;               // pixel of the wave's round (0..15)
+  const long long M = (long long)n * ho * wo;
+  const long long m0 = (long long)blockIdx.x * kD1Rows + wave * 256;
+  float K[8], s1[8], s2[8];
+  float cnt = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) K[k] = s1[k] = s2[k] = 0.f;
+  for (int rd = 0; rd < 16; ++rd) {
+    const long long m = m0 + rd * 16 + pl;
+    if (m >= M) break;                    // (rounds past the end: whole 16-pixel groups, wave-uniform per quad)
+    const int b = (int)(m / ((long long)ho * wo));
+    const int rem = (int)(m - (long long)b * ho * wo);
+    const int oh = rem / wo, ow = rem - oh * wo;
+    const TX* px = x + (((long long)b * h + 2 * oh) * w + 2 * ow) * xs;
+    float xv[9][4];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const TX* p = px + ((long long)r * w + c) * xs;
+        if constexpr (BF) {
+          const uint2 u = *reinterpret_cast<const uint2*>(p);     // channels 0..3 of the 8-wide pixel
+          xv[r * 3 + c][0] = bf2f(u.x & 0xffff); xv[r * 3 + c][1] = bf2f(u.x >> 16);
+          xv[r * 3 + c][2] = bf2f(u.y & 0xffff); xv[r * 3 + c][3] = bf2f(u.y >> 16);
+        } else {
+          const float4 u = *reinterpret_cast<const float4*>(p);
+          xv[r * 3 + c][0] = u.x; xv[r * 3 + c][1] = u.y; xv[r * 3 + c][2] = u.z; xv[r * 3 + c][3] = u.w;
+        }
+      }
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci) {
+        const float4 w0 = *reinterpret_cast<const float4*>(s_w + (tap * 4 + ci) * kD1Cout + 8 * g);
+        const float4 w1 = *reinterpret_cast<const float4*>(s_w + (tap * 4 + ci) * kD1Cout + 8 * g + 4);
+        const float a = xv[tap][ci];
+        acc[0] = fmaf(a, w0.x, acc[0]); acc[1] = fmaf(a, w0.y, acc[1]);
+        acc[2] = fmaf(a, w0.z, acc[2]); acc[3] = fmaf(a, w0.w, acc[3]);
+        acc[4] = fmaf(a, w1.x, acc[4]); acc[5] = fmaf(a, w1.y, acc[5]);
+        acc[6] = fmaf(a, w1.z, acc[6]); acc[7] = fmaf(a, w1.w, acc[7]);
+      }
+    TX* py = y + m * kD1Cout + 8 * g;
+    float v[8];
+    if constexpr (BF) {
+      uint32_t q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint16_t lo = f2bf(acc[2 * k]), hi = f2bf(acc[2 * k + 1]);
+        q[k] = (uint32_t)lo | ((uint32_t)hi << 16);
+        v[2 * k] = bf2f(lo);             // statistics of y as stored
+        v[2 * k + 1] = bf2f(hi);
+      }
+      *reinterpret_cast<uint4*>(py) = make_uint4(q[0], q[1], q[2], q[3]);
+    } else {
+      *reinterpret_cast<float4*>(py) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(py + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = acc[k];
+    }
+    if (stats) {
+      if (cnt == 0.f) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) K[k] = v[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = v[k] - K[k];
+        s1[k] += d;
+        s2[k] = fmaf(d, d, s2[k]);
+      }
+      cnt += 1.f;
+    }
+  }
+  if (!stats) return;
+  // per thread (n, mean, M2) of its pixels, then the 16 lanes of the channel
+  // group (xor 4, 8, 16, 32: lanes with equal lane & 3), then the 4 waves
+  float mu[8], q2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mu[k] = cnt > 0.f ? K[k] + s1[k] / cnt : 0.f;
+    q2[k] = cnt > 0.f ? fmaxf(s2[k] - s1[k] * s1[k] / cnt, 0.f) : 0.f;
+  }
+#pragma unroll
+  for (int o = 4; o < 64; o <<= 1) {
+    const float nb = __shfl_xor(cnt, o, 64);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float mb = __shfl_xor(mu[k], o, 64), qb = __shfl_xor(q2[k], o, 64);
+      float na = cnt;
+      chan_combine(na, mu[k], q2[k], nb, mb, qb);
+    }
+    cnt = cnt + nb;
+  }
+  if (pl == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s_red[0][wave][8 * g + k] = cnt;
+      s_red[1][wave][8 * g + k] = mu[k];
+      s_red[2][wave][8 * g + k] = q2[k];
+    }
+  }
+  __syncthreads();
+  if (t < kD1Cout) {
+    float na = s_red[0][0][t], ma = s_red[1][0][t], qa = s_red[2][0][t];
+    for (int wv = 1; wv < 4; ++wv) chan_combine(na, ma, qa, s_red[0][wv][t], s_red[1][wv][t], s_red[2][wv][t]);
+    stats[(long long)t * P + blockIdx.x] = ma;
+    stats[(long long)(kD1Cout + t) * P + blockIdx.x] = qa;
+  }
+}
+
+bool conv1_direct_ok(const jr_conv_desc* d, int dtype) {
+  static const bool on = [] {
+    const char* e = std::getenv("JR_CONV1_DIRECT");
+    return !(e && e[0] == '0');
+  }();
+  const int q = dtype == JR_BF16 ? 8 : 4;
+  return on && (dtype == JR_F32 || dtype == JR_F32_X8 || dtype == JR_BF16) && d->c_in <= 3 &&
+         d->x_c_stride == q && d->x_c_off == 0 && d->c_out == kD1Cout && d->y_c_off == 0 &&
+         d->y_c_stride == kD1Cout && d->kh == 3 && d->kw == 3 && d->stride_h == 2 && d->stride_w == 2 &&
+         d->pad_h == 0 && d->pad_w == 0;
+}
+
+int conv1_direct_partials(const jr_conv_desc* d, int* P, int* R) {
+  const long long M = (long long)d->n * d->ho * d->wo;
+  *R = kD1Rows;
+  *P = (int)ceil_div(M, kD1Rows);
+  return JR_OK;
+}
+
+void launch_conv1_direct(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y, float* stats,
+                         int members, long long x_mb, long long w_mb, long long y_mb, long long s_mb,
+                         hipStream_t s) {
+  int P, R;
+  conv1_direct_partials(d, &P, &R);
+  const dim3 grid((unsigned)P, (unsigned)members);
+  const int c8 = (d->c_in + 7) / 8 * 8;
+  if (dtype == JR_BF16)
+    hipLaunchKernelGGL((k_conv1_direct<uint16_t, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)x, d->x_c_stride,
+                       (const uint16_t*)w, (uint16_t*)y, d->n, d->h, d->w, d->ho, d->wo, d->c_in, c8, stats, P, x_mb,
+                       w_mb, y_mb, s_mb);
+  else
+    hipLaunchKernelGGL((k_conv1_direct<float, float>), grid, dim3(256), 0, s, (const float*)x, d->x_c_stride,
+                       (const float*)w, (float*)y, d->n, d->h, d->w, d->ho, d->wo, d->c_in, c8, stats, P, x_mb, w_mb,
+                       y_mb, s_mb);
+}
+
+}  // namespace jr

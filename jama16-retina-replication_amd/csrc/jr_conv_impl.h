@@ -573,6 +573,9 @@ __global__ void __launch_bounds__(256) k_splitk_reduce_stats(const float* __rest
 // (mean, invstd) per channel from stats[2][N][P] partials of R rows each
 // (jr_conv.hip; single-pass shifted combine in fp64, two stages when P is
 // large).
+__global__ void __launch_bounds__(256) k_stats_finalize8(const float* __restrict__ part, int P, int R, int M, int N,
+                                                         float eps, float* mean, float* invstd, long long p_mb,
+                                                         long long st_mb);
 __global__ void __launch_bounds__(256) k_stats_finalize(const float* __restrict__ part, const float* __restrict__ cnt,
                                                         int P, int R, int M, int N, int chunk, float eps,
                                                         float* mean, float* invstd, float* out, long long p_mb,
@@ -714,6 +717,13 @@ static constexpr HaloCfg kHaloBf16[] = {
 };
 constexpr int kNumHaloBf16 = sizeof(kHaloBf16) / sizeof(kHaloBf16[0]);
 void launch_conv_halo(int h, const ConvArgs& a, dim3 grid, hipStream_t s);
+// conv2d_1 as a direct VALU convolution (jr_conv_direct.hip): the geometry
+// test, its statistics partials (P of R rows) and the launch (stats may be
+// nullptr; members > 1: blockIdx.y, byte strides)
+bool conv1_direct_ok(const jr_conv_desc* d, int dtype);
+int conv1_direct_partials(const jr_conv_desc* d, int* P, int* R);
+void launch_conv1_direct(const jr_conv_desc* d, int dtype, const void* x, const void* w, void* y, float* stats,
+                         int members, long long x_mb, long long w_mb, long long y_mb, long long s_mb, hipStream_t s);
 
 // bf16-operand GEMM launch (jr_conv_bf16.hip): tile index into kCfgsBf16
 // (np = 1, JR_BF16) or kCfgsX8P (np = 3, JR_F32_X8P).

@@ -57,6 +57,12 @@ class WgradSeg(Structure):
         "m", "n", "splits", "c_in", "c_pad", "g", "block0", "blocks")]
 
 
+class BnPartials(Structure):
+    """include/jr.h jr_bn_partials: where a forward GEMM leaves its BN-statistics partials."""
+    _fields_ = [("ws_offset", c_int64), ("P", c_int32), ("R", c_int32), ("M", c_int32), ("N", c_int32),
+                ("single_stage", c_int32)]
+
+
 class PoolDesc(Structure):
     _fields_ = [(n, c_int32) for n in (
         "n", "h", "w", "c", "ho", "wo", "x_c_off", "x_c_stride", "y_c_off", "y_c_stride")]
@@ -72,6 +78,12 @@ _SIGS = {
                               c_size_t, c_void_p]),
     "jr_conv2d_fwd_bn_stats": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_float,
                                        c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "jr_conv2d_bn_partials_layout": (c_int, [POINTER(ConvDesc), c_int, POINTER(BnPartials)]),
+    "jr_conv2d_fwd_bn_partials": (c_int, [POINTER(ConvDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                          c_void_p]),
+    "jr_bn_relu_apply_stats": (c_int, [c_int, c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p, c_int32, c_int32,
+                                       c_int32, c_int32, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                       c_int32, c_void_p]),
     "jr_conv2d_workspace_size_grouped": (c_size_t, [POINTER(ConvDesc), c_int, c_int]),
     "jr_conv2d_fwd_bn_stats_grouped": (c_int, [POINTER(ConvDesc), c_int, c_int, c_void_p, c_int64, c_void_p, c_int64,
                                                c_void_p, c_int64, c_float, c_void_p, c_void_p, c_int64, c_void_p,

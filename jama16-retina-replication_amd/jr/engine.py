@@ -88,7 +88,8 @@ class Engine:
                  optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
                  head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None,
                  autotune: bool = False, tiles: str = "pinned", fuse_siblings: bool = True, lanes: int = 2,
-                 conv_math: Optional[str] = None, defer_wgrad: bool = True, fuse_pool: Optional[bool] = None):
+                 conv_math: Optional[str] = None, defer_wgrad: bool = True, fuse_pool: Optional[bool] = None,
+                 fold_stats: Optional[bool] = None):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if conv_math is None:            # fp32 default: x8 (fp32-accurate, on the bf16 matrix cores)
@@ -145,6 +146,16 @@ class Engine:
         if fuse_pool is None:           # (JR_FUSE_POOL=0: the separate apply + max-pool, for A/B runs)
             fuse_pool = os.environ.get("JR_FUSE_POOL", "1") != "0"
         self.pool_fused = fusable_pools(self.g, self.plan) if fuse_pool else {}
+        # the BN-statistics finalize folded into the BN apply for launches whose
+        # partials are single-stage and at most JR_FOLD_MAX_P per channel
+        # (jr_conv2d_fwd_bn_partials + jr_bn_relu_apply_stats: a kernel
+        # boundary fewer per layer; bitwise the separate finalize).  Opt-in
+        # (JR_FOLD_STATS=1): measured neutral, f32 and bf16
+        # (profiles/r05_ab_rows_{bf16,f32}.txt)
+        if fold_stats is None:
+            fold_stats = os.environ.get("JR_FOLD_STATS", "0") == "1"
+        self.fold_stats = bool(fold_stats)
+        self.fold_max_p = int(os.environ.get("JR_FOLD_MAX_P", "512"))
         self.cunits: List[ConvUnit] = self.plan.units
         self.layout, self.nparam = self.plan.layout, self.plan.nparam
         self._alloc()
@@ -580,6 +591,29 @@ class Engine:
                     add(fwd, L.jr_split_x8p, (A(u.x), rows, b.c, 0, src_stride, AX(u.x), cp, 0, cp,
                                               self.batch * b.h * b.w * cp, s),
                         "split_x8p", ln, a_all(u.x), [("ap", u.x)], nbytes=rows * (4 * b.c + 6 * cp))
+                lay = None
+                if self.fold_stats and not any(m.y.buf in fused_bufs for m in u.members):
+                    lay = _ffi.BnPartials()
+                    _ffi.check("jr_conv2d_bn_partials_layout",
+                               L.jr_conv2d_bn_partials_layout(ctypes.byref(d), cdt, ctypes.byref(lay)))
+                    if not lay.single_stage or lay.P > self.fold_max_p:
+                        lay = None
+                if lay is not None:
+                    # conv + the statistics partials; each member's BN apply
+                    # combines its channels' partials (and stores mean / invstd)
+                    add(fwd, L.jr_conv2d_fwd_bn_partials, (ctypes.byref(d), cdt, AX(u.x), self._wf(u), raw, ws, wsb,
+                                                           s),
+                        "conv_fwd", ln, ax_reads(u.x) + [wkey], [("r", uid), ("ws", ln)])
+                    part = ws.value + lay.ws_offset
+                    for m, co in zip(u.members, u.col_off):
+                        yb = g.bufs[m.y.buf]
+                        add(fwd, L.jr_bn_relu_apply_stats,
+                            (dt, raw, co, u.cout, M, m.cout, part, lay.P, lay.R, u.cout, co, BN_EPS,
+                             self.mean[m.idx].data_ptr(), self.invstd[m.idx].data_ptr(),
+                             self._p(f"batch_normalization_{m.idx + 1}/beta"), A(m.y.buf), m.y.c_off, yb.c, s),
+                            "bn_relu", ln, [("r", uid), ("ws", ln), ("p",)], [("a", m.y.buf, m.y.c_off), ("r", uid)],
+                            nbytes=2 * M * m.cout * self.esz)
+                    continue
                 # conv + the BN batch statistics of its raw output, fused
                 add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), cdt, AX(u.x), self._wf(u), raw, BN_EPS,
                                                     self.mean_unit[uid].data_ptr(),
