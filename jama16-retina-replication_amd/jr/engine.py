@@ -139,6 +139,12 @@ class Engine:
         self._fork_ev = torch.cuda.Event()
         self._join_ev = [torch.cuda.Event() for _ in range(self.nlanes - 1)]
         self._tail_ev = [torch.cuda.Event() for _ in range(self.nlanes)]
+        # eager runs: a cross-lane consumer waits for its producing call (an
+        # event recorded right after it) instead of the other lane's tail
+        # (JR_PRECISE_WAITS=0: tail waits, as captured graphs always use)
+        self.precise_waits = os.environ.get("JR_PRECISE_WAITS", "1") != "0"
+        self._prod_ev: Dict[int, torch.cuda.Event] = {}
+        self._capturing = False
         self.plan = build_plan(self.g, fuse_siblings)
         # conv2d_bn outputs read only by a max-pool (the stem's conv2d_3 and
         # conv2d_5): BN + ReLU run inside the pool (jr_bn_relu_maxpool3x3s2_fwd)
@@ -850,13 +856,26 @@ class Engine:
                     hook(c.args)
                 continue
             st = self.lane_streams[c.lane]
-            for lj in c.waits:              # the other lane's tail (jr.lanes.schedule)
-                ev = self._tail_ev[lj]
-                ev.record(self.lane_streams[lj])
-                st.wait_event(ev)
+            if self.precise_waits and not self._capturing:
+                for lj, j in c.pwaits:      # the producing call on the other lane (jr.lanes.schedule)
+                    ev = self._prod_ev.get(j)
+                    if ev is None:          # producer never run in this process (e.g. backward() first): its tail
+                        ev = self._tail_ev[lj]
+                        ev.record(self.lane_streams[lj])
+                    st.wait_event(ev)
+            else:
+                for lj in c.waits:          # the other lane's tail (jr.lanes.schedule)
+                    ev = self._tail_ev[lj]
+                    ev.record(self.lane_streams[lj])
+                    st.wait_event(ev)
             rc = c.fn(*c.args)
             if rc:
                 raise _ffi.JRError(c.name, rc, _ffi.last_error())
+            if c.record and self.precise_waits and not self._capturing:
+                ev = self._prod_ev.get(c.idx)
+                if ev is None:
+                    ev = self._prod_ev[c.idx] = torch.cuda.Event()
+                ev.record(st)
 
     def _fork(self) -> None:
         """Every lane waits for the work enqueued on lane 0 so far."""
@@ -966,6 +985,7 @@ class Engine:
         fwd, bwd, opt, _, _ = self._build_calls(B)
         torch.cuda.synchronize(self.device)
         _ffi.check("jr_graph_begin", self.lib.jr_graph_begin(self._s))
+        self._capturing = True
         try:
             self._fork()
             self._run(fwd)
@@ -974,6 +994,7 @@ class Engine:
             self._join()
             self._run(opt)
         finally:
+            self._capturing = False
             ex = ctypes.c_void_p()
             _ffi.check("jr_graph_end", self.lib.jr_graph_end(self._s, ctypes.byref(ex)))
         self._graphs[B] = ex.value

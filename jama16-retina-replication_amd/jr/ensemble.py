@@ -81,6 +81,8 @@ class EnsembleEngine:
         self._fork_ev = torch.cuda.Event()
         self._join_ev = [torch.cuda.Event() for _ in range(self.nlanes - 1)]
         self._tail_ev = [torch.cuda.Event() for _ in range(self.nlanes)]
+        self.precise_waits = os.environ.get("JR_PRECISE_WAITS", "1") != "0"   # (jr.Engine)
+        self._prod_ev = {}
         self._alloc()
         self.load_params(params)
         self.tiles = "heuristic"
@@ -329,13 +331,22 @@ class EnsembleEngine:
                 st.wait_event(self._fork_ev)
         for c in calls:
             st = self.lane_streams[c.lane]
-            for lj in c.waits:       # the other lane's tail (jr.lanes.schedule)
-                ev = self._tail_ev[lj]
-                ev.record(self.lane_streams[lj])
-                st.wait_event(ev)
+            if self.precise_waits:
+                for _, j in c.pwaits:    # the producing call on the other lane (jr.lanes.schedule)
+                    st.wait_event(self._prod_ev[j])   # (one call list: producers always ran first)
+            else:
+                for lj in c.waits:       # the other lane's tail
+                    ev = self._tail_ev[lj]
+                    ev.record(self.lane_streams[lj])
+                    st.wait_event(ev)
             rc = c.fn(*c.args)
             if rc:
                 raise _ffi.JRError(c.name, rc, _ffi.last_error())
+            if c.record and self.precise_waits:
+                ev = self._prod_ev.get(c.idx)
+                if ev is None:
+                    ev = self._prod_ev[c.idx] = torch.cuda.Event()
+                ev.record(st)
         for ev, st in zip(self._join_ev, self.lane_streams[1:]):    # join onto lane 0
             ev.record(st)
             self.stream.wait_event(ev)

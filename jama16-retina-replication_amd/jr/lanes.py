@@ -21,7 +21,8 @@ edges).
   call waits for the last writer of what it reads or writes and for the
   readers since that write of what it writes (RAW, WAW, WAR) -- when those run
   on another lane (by waiting for that lane's tail); same-lane order is
-  stream order.  Accumulating writers of
+  stream order.  (Eager runs wait for the producing call itself instead of
+  the other lane's tail: Call.pwaits.)  Accumulating writers of
   one gradient buffer are therefore serialised in issue order, so the result
   is bitwise the single-stream result.
 """
@@ -42,6 +43,12 @@ class Call:
     idx: int = -1                                   # position in the step's call sequence
     waits: List[int] = field(default_factory=list)  # lanes whose work so far must finish first
     nbytes: int = 0                                 # algorithmic HBM bytes (memory-bound ops; bench.py)
+    # producer waits (eager runs): (lane, call index) pairs -- wait for THAT
+    # call of the other lane (an event recorded right after it), not for
+    # everything the host had issued there by then; record: this call is
+    # such a producer
+    pwaits: List[Tuple[int, int]] = field(default_factory=list)
+    record: bool = False
 
 
 def node_lanes(g, plan, nl: int) -> Dict[int, int]:
@@ -88,9 +95,12 @@ def schedule(calls: Sequence[Call]) -> None:
     readers: Dict[object, List[int]] = {}
     tail: Dict[int, int] = {}                       # lane -> newest call issued on it
     synced: Dict[Tuple[int, int], int] = {}         # (lane, other lane) -> other lane's tail when last waited for
+    psynced: Dict[Tuple[int, int], int] = {}        # the same for the producer waits
     for i, c in enumerate(calls):
         c.idx = i
         c.waits = []
+        c.pwaits = []
+        c.record = False
     for i, c in enumerate(calls):
         dep = set()
         for k in c.reads:
@@ -111,6 +121,10 @@ def schedule(calls: Sequence[Call]) -> None:
             if lj != c.lane:
                 need[lj] = max(need.get(lj, -1), j)
         for lj, j in sorted(need.items()):
+            if psynced.get((c.lane, lj), -1) < j:   # (a wait for j' >= j on lane lj covers j)
+                psynced[(c.lane, lj)] = j
+                c.pwaits.append((lj, j))
+                calls[j].record = True
             if synced.get((c.lane, lj), -1) >= j:
                 continue                            # already waited for a tail at or past j
             synced[(c.lane, lj)] = tail[lj]
@@ -118,9 +132,10 @@ def schedule(calls: Sequence[Call]) -> None:
         tail[c.lane] = i
 
 
-def check_schedule(calls: Sequence[Call]) -> None:
+def check_schedule(calls: Sequence[Call], precise: bool = False) -> None:
     """Test helper: every pair of conflicting calls on different lanes is
-    ordered by a chain of same-lane order and tail waits (happens-before)."""
+    ordered by a chain of same-lane order and tail waits (precise: producer
+    waits) -- happens-before."""
     hb: List[Dict[int, int]] = []
     last_on_lane: Dict[int, int] = {}
     for i, c in enumerate(calls):
@@ -129,11 +144,14 @@ def check_schedule(calls: Sequence[Call]) -> None:
         if prev is not None:
             known = dict(hb[prev])
             known[c.lane] = max(known.get(c.lane, -1), prev)
-        for lj in c.waits:
+        targets = ([(lj, j) for lj, j in c.pwaits] if precise
+                   else [(lj, last_on_lane.get(lj)) for lj in c.waits])
+        for lj, t in targets:
             assert lj != c.lane
-            t = last_on_lane.get(lj)
             if t is None:
                 continue
+            if precise:
+                assert calls[t].lane == lj and calls[t].record and t < i
             for l2, k in hb[t].items():
                 known[l2] = max(known.get(l2, -1), k)
             known[lj] = max(known.get(lj, -1), t)

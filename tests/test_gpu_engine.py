@@ -213,6 +213,7 @@ def test_lanes_are_bitwise_single_stream(dtype):
     fwd, bwd, opt, _, _ = many._build_calls(4)
     seq = sorted([c for c in fwd + bwd + opt if c.idx >= 0], key=lambda c: c.idx)
     check_schedule(seq)
+    check_schedule(seq, precise=True)
     assert len({c.lane for c in seq}) == 4
     with pytest.raises(ValueError):
         many.capture()

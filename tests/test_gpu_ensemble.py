@@ -216,6 +216,7 @@ def test_ensemble_lanes_are_bitwise_one_lane(dtype, res, B):
     for n in (B, 5):
         calls, _ = two._build_calls(n)
         check_schedule(calls)
+        check_schedule(calls, precise=True)
         assert {c.lane for c in calls} == {0, 1}
         for k in range(3):
             x = synth.fundus_batch(700 + 40 * k, n, res)

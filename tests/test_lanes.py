@@ -39,6 +39,7 @@ def test_schedule_random_sequences_are_race_free():
             calls.append(Call(None, (), f"c{i}", rng.randint(0, 3), tuple(res), tuple(wr)))
         schedule(calls)
         check_schedule(calls)
+        check_schedule(calls, precise=True)
 
 
 def test_schedule_serialises_accumulating_writers_in_issue_order():
@@ -47,7 +48,9 @@ def test_schedule_serialises_accumulating_writers_in_issue_order():
              Call(None, (), "w2", 3, (), (("d", 5, 0),)), Call(None, (), "r", 0, (("d", 5, 0),), ())]
     schedule(calls)
     check_schedule(calls)
+    check_schedule(calls, precise=True)
     assert calls[1].waits == [1] and calls[2].waits == [2] and calls[3].waits == [3]
+    assert calls[1].pwaits == [(1, 0)] and calls[2].pwaits == [(2, 1)] and calls[3].pwaits == [(3, 2)]
 
 
 def test_schedule_skips_waits_already_implied():
@@ -55,4 +58,17 @@ def test_schedule_skips_waits_already_implied():
              Call(None, (), "c", 0, (("x",),), (("z",),))]
     schedule(calls)
     assert calls[1].waits == [1] and calls[2].waits == []   # lane 0 already waited for lane 1's tail
+    assert calls[1].pwaits == [(1, 0)] and calls[2].pwaits == [] and calls[0].record
     check_schedule(calls)
+    check_schedule(calls, precise=True)
+
+
+def test_producer_waits_do_not_wait_for_later_work():
+    # lane 1 issues a (producer) then b (unrelated); lane 0's consumer of a
+    # waits for a itself, while the tail wait covers b too
+    calls = [Call(None, (), "a", 1, (), (("x",),)), Call(None, (), "b", 1, (), (("y",),)),
+             Call(None, (), "c", 0, (("x",),), (("z",),))]
+    schedule(calls)
+    assert calls[2].waits == [1] and calls[2].pwaits == [(1, 0)]
+    assert calls[0].record and not calls[1].record
+    check_schedule(calls, precise=True)
