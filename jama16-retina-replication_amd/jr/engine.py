@@ -145,6 +145,10 @@ class Engine:
         self.precise_waits = os.environ.get("JR_PRECISE_WAITS", "1") != "0"
         self._prod_ev: Dict[int, torch.cuda.Event] = {}
         self._capturing = False
+        # backward order per conv launch: the data gradient (the critical
+        # path to the next layer's BN backward) before the filter gradient
+        # (JR_DGRAD_FIRST=0: filter gradient first)
+        self.dgrad_first = os.environ.get("JR_DGRAD_FIRST", "1") != "0"
         self.plan = build_plan(self.g, fuse_siblings)
         # conv2d_bn outputs read only by a max-pool (the stem's conv2d_3 and
         # conv2d_5): BN + ReLU run inside the pool (jr_bn_relu_maxpool3x3s2_fwd)
@@ -784,6 +788,14 @@ class Engine:
                         add(bwd, L.jr_split_x8p, (draw, M, u.cout, 0, u.cout, drawp, u.cout, 0, u.cout, M * u.cout, s),
                             "split_x8p", ln, [("draw", ln)], [("drawp", ln)], nbytes=10 * M * u.cout)
                         draw, dkey = drawp, ("drawp", ln)
+                    def dgrad():
+                        if u.x != g.input_buf:
+                            add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), cdt, draw, self._wd(u), D(u.x), acc, ws,
+                                                            wsb, s),
+                                "conv_dgrad", ln, [dkey, wkey], d_all(u.x) + [("ws", ln)])
+                            written.add(u.x)
+                    if self.dgrad_first:
+                        dgrad()
                     if uid in defer:
                         sg, _, nb = defer[uid]
                         add(bwd, L.jr_conv2d_bwd_filter_slabs, (ctypes.byref(d), cdt, AX(u.x), draw, sg.slabs, nb,
@@ -799,11 +811,8 @@ class Engine:
                         add(bwd, L.jr_conv2d_bwd_filter, (ctypes.byref(d), cdt, AX(u.x), draw,
                                                           self.grads.data_ptr() + 4 * u.koff, ws, wsb, s),
                             "conv_wgrad", ln, ax_reads(u.x) + [dkey], [("g", uid), ("ws", ln)])
-                    if u.x != g.input_buf:
-                        add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), cdt, draw, self._wd(u), D(u.x), acc, ws, wsb,
-                                                        s),
-                            "conv_dgrad", ln, [dkey, wkey], d_all(u.x) + [("ws", ln)])
-                        written.add(u.x)
+                    if not self.dgrad_first:
+                        dgrad()
                     trigger = False
                     while flush_at and flush_at[0] >= u.koff:
                         flush_at.pop(0)
