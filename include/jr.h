@@ -440,6 +440,17 @@ int jr_graph_destroy(void* graph_exec);
  * flags of captured conv GEMMs) and released by jr_graph_destroy (tests). */
 int jr_graph_regions(void* graph_exec);
 
+/* ---- Cross-stream ordering of the branch lanes ---------------------- */
+/* Events for device-side ordering between the library's callers' streams
+ * (jr.lanes: a consumer on one lane waits for its producer on another):
+ * no timing and no system-scope fence -- device memory only, the only
+ * thing the lanes order.  (A recorded DisableSystemFence event costs the
+ * producer's queue ~1.1 us less than a default one: profiles/r05_sync_probe2.txt.) */
+int jr_event_create(void** event);
+int jr_event_record(void* event, void* stream);
+int jr_stream_wait_event(void* stream, void* event);
+int jr_event_destroy(void* event);
+
 #ifdef __cplusplus
 }
 #endif

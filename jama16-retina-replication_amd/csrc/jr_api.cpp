@@ -243,3 +243,27 @@ JR_API int jr_graph_regions(void* graph_exec) {
   auto it = g_graph_regions.find(reinterpret_cast<hipGraphExec_t>(graph_exec));
   return it == g_graph_regions.end() ? 0 : (int)it->second.size();
 }
+
+JR_API int jr_event_create(void** event) {
+  if (!event) return fail(JR_ERR_INVALID, "event_create: null handle pointer");
+  hipEvent_t e = nullptr;
+  const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence);
+  if (r != hipSuccess) return fail(JR_ERR_HIP, std::string("event_create: ") + hipGetErrorString(r));
+  *event = e;
+  return JR_OK;
+}
+
+JR_API int jr_event_record(void* event, void* stream) {
+  const hipError_t r = hipEventRecord(reinterpret_cast<hipEvent_t>(event), as_stream(stream));
+  return r == hipSuccess ? JR_OK : fail(JR_ERR_HIP, std::string("event_record: ") + hipGetErrorString(r));
+}
+
+JR_API int jr_stream_wait_event(void* stream, void* event) {
+  const hipError_t r = hipStreamWaitEvent(as_stream(stream), reinterpret_cast<hipEvent_t>(event), 0);
+  return r == hipSuccess ? JR_OK : fail(JR_ERR_HIP, std::string("stream_wait_event: ") + hipGetErrorString(r));
+}
+
+JR_API int jr_event_destroy(void* event) {
+  const hipError_t r = hipEventDestroy(reinterpret_cast<hipEvent_t>(event));
+  return r == hipSuccess ? JR_OK : fail(JR_ERR_HIP, std::string("event_destroy: ") + hipGetErrorString(r));
+}

@@ -175,6 +175,10 @@ _SIGS = {
     "jr_graph_launch": (c_int, [c_void_p, c_void_p]),
     "jr_graph_destroy": (c_int, [c_void_p]),
     "jr_graph_regions": (c_int, [c_void_p]),
+    "jr_event_create": (c_int, [ctypes.POINTER(c_void_p)]),
+    "jr_event_record": (c_int, [c_void_p, c_void_p]),
+    "jr_stream_wait_event": (c_int, [c_void_p, c_void_p]),
+    "jr_event_destroy": (c_int, [c_void_p]),
     "jr_device_check": (c_int, []),
     "jr_debug_set_sk_spin_limit": (c_int, [ctypes.c_uint32]),
 }

@@ -27,6 +27,7 @@ import ctypes
 import dataclasses
 import json
 import os
+import weakref
 from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
@@ -136,6 +137,7 @@ class Engine:
         self.nlanes = max(1, int(lanes))
         self.lane_streams = [self.stream] + [torch.cuda.Stream(device=self.device, priority=prio[i])
                                              for i in range(1, self.nlanes)]
+        self._lane_s = [ctypes.c_void_p(st.cuda_stream) for st in self.lane_streams]
         self._fork_ev = torch.cuda.Event()
         self._join_ev = [torch.cuda.Event() for _ in range(self.nlanes - 1)]
         self._tail_ev = [torch.cuda.Event() for _ in range(self.nlanes)]
@@ -143,7 +145,10 @@ class Engine:
         # event recorded right after it) instead of the other lane's tail
         # (JR_PRECISE_WAITS=0: tail waits, as captured graphs always use)
         self.precise_waits = os.environ.get("JR_PRECISE_WAITS", "1") != "0"
-        self._prod_ev: Dict[int, torch.cuda.Event] = {}
+        self._prod_ev: Dict[int, object] = {}
+        # producer events: libjr's (no timing, no system-scope fence: cheaper
+        # to record) or torch's (JR_LANE_EVENTS=torch, for A/B runs)
+        self._native_ev = os.environ.get("JR_LANE_EVENTS", "native") != "torch"
         self._capturing = False
         # backward order per conv launch: the data gradient (the critical
         # path to the next layer's BN backward) before the filter gradient
@@ -871,7 +876,11 @@ class Engine:
                     if ev is None:          # producer never run in this process (e.g. backward() first): its tail
                         ev = self._tail_ev[lj]
                         ev.record(self.lane_streams[lj])
-                    st.wait_event(ev)
+                        st.wait_event(ev)
+                    elif self._native_ev:
+                        _ffi.check("jr_stream_wait_event", self.lib.jr_stream_wait_event(self._lane_s[c.lane], ev))
+                    else:
+                        st.wait_event(ev)
             else:
                 for lj in c.waits:          # the other lane's tail (jr.lanes.schedule)
                     ev = self._tail_ev[lj]
@@ -883,8 +892,19 @@ class Engine:
             if c.record and self.precise_waits and not self._capturing:
                 ev = self._prod_ev.get(c.idx)
                 if ev is None:
-                    ev = self._prod_ev[c.idx] = torch.cuda.Event()
-                ev.record(st)
+                    ev = self._prod_ev[c.idx] = self._new_event()
+                if self._native_ev:
+                    _ffi.check("jr_event_record", self.lib.jr_event_record(ev, self._lane_s[c.lane]))
+                else:
+                    ev.record(st)
+
+    def _new_event(self):
+        if not self._native_ev:
+            return torch.cuda.Event()
+        ev = ctypes.c_void_p()
+        _ffi.check("jr_event_create", self.lib.jr_event_create(ctypes.byref(ev)))
+        weakref.finalize(self, self.lib.jr_event_destroy, ev)
+        return ev
 
     def _fork(self) -> None:
         """Every lane waits for the work enqueued on lane 0 so far."""

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from typing import List, Optional
 
 import numpy as np
@@ -82,7 +83,8 @@ class EnsembleEngine:
         self._join_ev = [torch.cuda.Event() for _ in range(self.nlanes - 1)]
         self._tail_ev = [torch.cuda.Event() for _ in range(self.nlanes)]
         self.precise_waits = os.environ.get("JR_PRECISE_WAITS", "1") != "0"   # (jr.Engine)
-        self._prod_ev = {}
+        self._prod_ev = {}               # libjr events (jr_event_create), as jr.Engine's
+        self._lane_s = [ctypes.c_void_p(st.cuda_stream) for st in self.lane_streams]
         self._alloc()
         self.load_params(params)
         self.tiles = "heuristic"
@@ -333,7 +335,9 @@ class EnsembleEngine:
             st = self.lane_streams[c.lane]
             if self.precise_waits:
                 for _, j in c.pwaits:    # the producing call on the other lane (jr.lanes.schedule)
-                    st.wait_event(self._prod_ev[j])   # (one call list: producers always ran first)
+                    # (one call list: producers always ran first)
+                    _ffi.check("jr_stream_wait_event", self.lib.jr_stream_wait_event(self._lane_s[c.lane],
+                                                                                     self._prod_ev[j]))
             else:
                 for lj in c.waits:       # the other lane's tail
                     ev = self._tail_ev[lj]
@@ -345,8 +349,10 @@ class EnsembleEngine:
             if c.record and self.precise_waits:
                 ev = self._prod_ev.get(c.idx)
                 if ev is None:
-                    ev = self._prod_ev[c.idx] = torch.cuda.Event()
-                ev.record(st)
+                    ev = self._prod_ev[c.idx] = ctypes.c_void_p()
+                    _ffi.check("jr_event_create", self.lib.jr_event_create(ctypes.byref(ev)))
+                    weakref.finalize(self, self.lib.jr_event_destroy, ev)
+                _ffi.check("jr_event_record", self.lib.jr_event_record(ev, self._lane_s[c.lane]))
         for ev, st in zip(self._join_ev, self.lane_streams[1:]):    # join onto lane 0
             ev.record(st)
             self.stream.wait_event(ev)
