@@ -56,7 +56,7 @@ def parse():
                          "(TFRecord read + JPEG decode + every member's forward) over synthetic records")
     ap.add_argument("--members", type=int, default=10, help="ensemble mode: members resident on the GPU")
     ap.add_argument("--images", type=int, default=2048, help="ensemble mode: synthetic test images")
-    ap.add_argument("--ens-lanes", type=int, default=1,
+    ap.add_argument("--ens-lanes", type=int, default=2,
                     help="ensemble mode: branch lanes of the grouped EnsembleEngine (each with its own workspace)")
     ap.add_argument("--per-member", action="store_true",
                     help="ensemble mode: one engine per member instead of the grouped EnsembleEngine")

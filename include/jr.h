@@ -97,16 +97,18 @@ const char* jr_version(void);
 /* Device-side failures of the launches on the CURRENT device since the last
  * check (call it after synchronising the streams that ran them): JR_OK, or
  * JR_ERR_DEVICE when a kernel counted a failure into the library's device
- * error word -- today the stream-K hand-off of a conv GEMM whose owner block
- * gave up waiting for a later piece's partial (its output is then invalid).
- * On JR_ERR_DEVICE the call synchronises the device, re-zeroes every
- * stream-K hand-off flag and the word, so the NEXT launches are correct.
- * Host-synchronising (one 4-byte copy; the repair path a device sync). */
+ * error word -- today a stream-K hand-off count found past its tile's piece
+ * count (a hand-off word that was not left zero; the tile's output is then
+ * invalid).  Stream-K blocks never wait for one another, so no timeout
+ * exists.  On JR_ERR_DEVICE the call synchronises the device, re-zeroes every
+ * stream-K hand-off word and the error word, so the NEXT launches are
+ * correct.  Host-synchronising (one 4-byte copy; the repair path a device
+ * sync). */
 int jr_device_check(void);
-/* Diagnostics: the stream-K owner's poll bound for later launches (default
- * 2^22 polls, ~1 s; 0 = never wait, every unpublished partial is a failure).
- * Process-wide. */
-int jr_debug_set_sk_spin_limit(uint32_t spins);
+/* Diagnostics (tests): set every stream-K hand-off word of `stream` (the
+ * current device's) to `value`, in stream order -- the next stream-K launch
+ * there then miscounts and must be reported by jr_device_check. */
+int jr_debug_poison_sk_counts(void* stream, uint32_t value);
 
 /* ---- convolution (train.py:129-130 -> Keras Conv2D -> TF Conv2D,
  *      Conv2DBackpropInput, Conv2DBackpropFilter created by .minimize at

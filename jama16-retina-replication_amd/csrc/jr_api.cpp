@@ -30,7 +30,6 @@ std::map<hipGraphExec_t, std::vector<void*>> g_graph_regions;
 
 constexpr int kMaxDevices = 64;
 unsigned* g_err_word[kMaxDevices] = {};
-std::atomic<unsigned> g_sk_spins{1u << 22};
 
 unsigned* scratch_alloc(hipStream_t s, size_t words) {
   void* p = nullptr;
@@ -103,8 +102,6 @@ unsigned* device_error_word() {
   return err_word_init(dev) == JR_OK ? g_err_word[dev] : nullptr;
 }
 
-unsigned sk_spin_limit() { return g_sk_spins.load(std::memory_order_relaxed); }
-
 int check_launch(const char* what) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(JR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -146,8 +143,8 @@ JR_API int jr_device_check(void) {
   hipError_t e = hipMemcpy(&h, w, sizeof(unsigned), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("jr_device_check: ") + hipGetErrorString(e));
   if (h == 0) return JR_OK;
-  // repair: every launch (and every late publisher) has finished, then the
-  // hand-off flags of every stream of this device and the word go back to 0
+  // repair: every launch has finished, then the hand-off words of every
+  // stream of this device and the error word go back to 0
   e = hipDeviceSynchronize();
   if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("jr_device_check: ") + hipGetErrorString(e));
   {
@@ -159,13 +156,20 @@ JR_API int jr_device_check(void) {
   (void)hipMemset(w, 0, sizeof(unsigned));
   (void)hipDeviceSynchronize();
   return fail(JR_ERR_DEVICE, "stream-K hand-off: " + std::to_string(h) +
-                                 " partial tile(s) not published within the owner's poll bound; the outputs of the "
-                                 "launches since the last jr_device_check are invalid (hand-off flags reset)");
+                                 " count(s) found past their tile's piece count (a hand-off word not left zero); the "
+                                 "outputs of the launches since the last jr_device_check are invalid (hand-off words "
+                                 "reset)");
 }
 
-JR_API int jr_debug_set_sk_spin_limit(uint32_t spins) {
-  g_sk_spins.store(spins, std::memory_order_relaxed);
-  return JR_OK;
+JR_API int jr_debug_poison_sk_counts(void* stream, uint32_t value) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(JR_ERR_HIP, "debug_poison_sk_counts: no current device");
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  auto it = g_scratch.find(std::make_tuple(dev, as_stream(stream), 0));
+  if (it == g_scratch.end() || !it->second.p) return fail(JR_ERR_INVALID, "debug_poison_sk_counts: no hand-off words on this stream yet");
+  const hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(it->second.p), (int)value, it->second.words,
+                                         as_stream(stream));
+  return e == hipSuccess ? JR_OK : fail(JR_ERR_HIP, std::string("debug_poison_sk_counts: ") + hipGetErrorString(e));
 }
 
 JR_API int jr_graph_begin(void* stream) {

@@ -27,8 +27,6 @@ unsigned* stream_scratch(hipStream_t s, int kind, size_t words);
 // failures into it (vector atomics); jr_device_check() reads, reports and
 // clears it.  Allocated by jr_init (or on first use outside a capture).
 unsigned* device_error_word();
-// Stream-K owner poll bound (jr_debug_set_sk_spin_limit; default 2^22).
-unsigned sk_spin_limit();
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

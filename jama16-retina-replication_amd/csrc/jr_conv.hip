@@ -137,17 +137,17 @@ struct SplitFrag {
 // equal contiguous ranges, one per block (g.sk_ipb each), so every CU gets
 // the same MAC count whatever the tile count -- no wave quantization and no
 // split-K slabs or reduce launch.  A block walks its range tile by tile; a
-// tile cut between blocks b < b' is finished by the block holding its FIRST
-// K-tile (b, at the END of its range): every later piece is the FIRST
-// segment of blocks b+1, b+2, ..., which publish it at the START of their
-// range as an fp32 partial (write-through sc1 stores, drained, then an
-// agent-scope flag), and b adds them in block order (deterministic: the
-// cut points are fixed by the grid, the sum order by the block order) before
-// its ordinary epilogue (store + fused BN statistics).  Waits point only to
-// higher blocks, which publish before waiting on anything, so no block waits
-// on one that cannot start; spins are bounded.  The flags are per-stream
-// library words (stream_scratch) that the consuming block resets, so a launch
-// needs no memset (one fill-kernel dispatch per stream-K GEMM before).
+// tile cut between blocks b < b+1 < ... (b holds its FIRST K-tile at the END
+// of its range, the later blocks its later K-tiles at the START of theirs)
+// is handed off without any block waiting (jr_conv_impl.h sk_handoff): each
+// piece is published as an fp32 partial (write-through sc1 stores, drained)
+// and counted on b's word, and the block completing the count adds the
+// pieces in block order (deterministic: the cut points are fixed by the
+// grid, the sum order by the block order) and runs the ordinary epilogue
+// (store + fused BN statistics).  No block depends on another being resident,
+// so concurrent kernels on other lanes or processes cannot stall a grid.  The
+// count words are per-stream library words (stream_scratch) that the
+// completing block resets, so a launch needs no memset.
 template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0, bool SK = false>
 __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int WGN = 4 / WGM;
@@ -672,15 +672,10 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   JR_ST(stamp.loop();)
 
   if constexpr (SK) {
-    const bool first = sk_first;
     sk_first = false;
-    if (kt0 != 0) {                  // (only a block's first segment starts inside a tile)
-      if (first) sk_publish<TM, TN>(g, acc, wave, lane);
-      continue;
-    }
-    // the tile's later pieces: the first segments of blocks blockIdx.x + 1, ...
-    for (int b = blockIdx.x + 1, covered = kt1; covered < g.ktiles; ++b, covered += (int)g.sk_ipb)
-      sk_absorb<TM, TN>(g, acc, b, wave, lane);
+    int owner, npieces, kind;
+    if (sk_cut(g, tile, kt0, kt1, &owner, &npieces, &kind) && !sk_handoff<TM, TN>(g, acc, wave, lane, owner, npieces, kind))
+      continue;                      // another block finishes the tile
   }
   // ---------------------------------------------------------------- epilogue
   conv_epilogue<OP, WM, TM, TN, false>(g, acc, smem + wave * stage_floats<WN>(), m0 + wm0, n0 + wn0, lane);
@@ -843,7 +838,7 @@ static Plan plan_with(int dtype, int cfg, int M, int N, int K, int op) {
     p.sk = true;
     p.sk_ipb = ceil_div(W, P);
     p.sk_blocks = (int)ceil_div(W, p.sk_ipb);
-    p.sk_slot = t.bm * t.bn;
+    p.sk_slot = t.bm * t.bn;   // two per block: the first segment's piece and the owner's last
   }
   p.kt_per_split = (int)ceil_div(std::max(p.ktiles, 1), splits);
   p.splits = (int)ceil_div(std::max(p.ktiles, 1), p.kt_per_split);
@@ -911,7 +906,7 @@ static int reduce_lanes(const Plan& p) {
 // stream-K: one BM x BN fp32 partial slot per block (the hand-off flags are
 // stream_scratch words)
 static size_t plan_ws(const Plan& p) {
-  if (p.sk) return (size_t)p.sk_blocks * p.sk_slot * sizeof(float);
+  if (p.sk) return 2 * (size_t)p.sk_blocks * p.sk_slot * sizeof(float);
   return p.splits > 1 ? (size_t)p.splits * (size_t)p.M * (size_t)p.N * sizeof(float) : 0;
 }
 
@@ -1149,10 +1144,9 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     a.sk_flags = stream_scratch(s, 0, (size_t)p.sk_blocks * members);
     if (!a.sk_flags) return fail(JR_ERR_HIP, "conv: stream-K flag words could not be allocated");
     a.sk_fmb = (long long)p.sk_blocks * sizeof(unsigned);
-    // a timed-out owner counts itself here instead of adding an unpublished slot
+    // a hand-off count found past its piece count (a word not left zero) is reported here
     a.sk_err = device_error_word();
     if (!a.sk_err) return fail(JR_ERR_HIP, "conv: no device error word (call jr_init before capturing)");
-    a.sk_spins = sk_spin_limit();
     grid = dim3(p.sk_blocks, members, 1);
   }
   if (is_halo(dtype, p.tile)) {

@@ -514,14 +514,11 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
   JR_ST(stamp.loop();)
 
   if constexpr (SK) {
-    const bool first = sk_first;
     sk_first = false;
-    if (kt0 != 0) {                  // (only a block's first segment starts inside a tile)
-      if (first) sk_publish<TM, TN, NW>(g, acc, wave, lane);
-      continue;
-    }
-    for (int b = blockIdx.x + 1, covered = kt1; covered < g.ktiles; ++b, covered += (int)g.sk_ipb)
-      sk_absorb<TM, TN, NW>(g, acc, b, wave, lane);
+    int owner, npieces, kind;
+    if (sk_cut(g, tile, kt0, kt1, &owner, &npieces, &kind) &&
+        !sk_handoff<TM, TN, NW>(g, acc, wave, lane, owner, npieces, kind))
+      continue;                      // another block finishes the tile
   }
   // ---------------------------------------------------------------- epilogue
   conv_epilogue<OP, WM, TM, TN, NP == 1>(g, acc, reinterpret_cast<float*>(smem) + wave * stage_floats<WN>(), m0 + wm0,

@@ -47,16 +47,15 @@ struct ConvArgs {
   // the statistics partials and the final output (split-K reduce)
   long long a_mb, b_mb, c_mb, s_mb, o_mb;
   // stream-K (jr_conv.hip k_conv SK): iterations (tile-major, K-tile-minor)
-  // per block, the per-block hand-off flags (stream_scratch words: zero at
-  // launch, and every flag set is reset by the block that consumes it) and
-  // the partial-tile slots (workspace); sk_fmb / sk_mb = their member strides
+  // per block, the per-owner-block hand-off counts (stream_scratch words:
+  // zero at launch, and the block that completes a count resets it) and the
+  // partial-tile slots (workspace, two per block); sk_fmb / sk_mb = their
+  // member strides
   long long sk_ipb, sk_mb, sk_fmb;
   unsigned* sk_flags;
   float* sk_part;
-  // the library's device error word (jr_device_check) and the owner's poll
-  // bound (jr_debug_set_sk_spin_limit; 0 = never wait)
+  // the library's device error word (jr_device_check)
   unsigned* sk_err;
-  unsigned sk_spins;
 };
 
 // Moves a grouped GEMM's operand / output pointers to member blockIdx.y
@@ -170,87 +169,141 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_chunk) {
 }
 
 // ---------------------------------------------------------------- stream-K
-// Hand-off of a cut tile's later pieces (jr_conv.hip k_conv SK documents the
-// scheme; k_conv_bf16 uses the same): write-through partials + one flag per
-// block, the owner's relaxed poll and sc1 loads.
+// Hand-off of a cut tile's pieces (jr_conv.hip k_conv SK documents the
+// scheme; k_conv_bf16 uses the same).  No block ever waits for another:
+// every piece is published to its block's slot (write-through sc1 stores,
+// drained) and then counted on the tile's word (one per owner block, the
+// block holding the tile's first K-tile); the block whose count completes
+// the tile adds the pieces in block order -- the owner's first -- and
+// finishes the tile, the others move on.  (Round 4's owner polled for the
+// later pieces: with two lanes, or two processes, sharing the CUs a grid's
+// later blocks need not be resident, and owners spun until their bound --
+// an error raised by jr_device_check, seen on the 2-rank one-device eval.)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t sk_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
 
+// Returns true in the block that finishes the tile, with acc = the sum of
+// the npieces pieces of blocks owner, owner + 1, ... in that order (each
+// piece's fp32 values exactly as its block accumulated them: bitwise the
+// owner-absorbs order of round 4).  kind: 1 = this is the owner's piece (its
+// last segment, starting at K-tile 0), 0 = a later block's (its first
+// segment).  The owner's word counts published pieces (low 16 bits) plus an
+// owner bit: the owner first only probes -- when every later piece is
+// already published (the usual case: later blocks publish at the START of
+// their ranges, the owner reaches its piece at the END of its range) it
+// finishes from its registers without publishing; otherwise it publishes and
+// counts like any piece.  A count found past npieces (a word not left zero)
+// goes to the device error word (jr_device_check).
 template <int TM, int TN, int NW = 4>
-__device__ __forceinline__ void sk_publish(const ConvArgs& g, const f32x16 (&acc)[TM][TN], int wave, int lane) {
-  constexpr int SLOT = NW * TM * TN * 16 * 64;              // floats per block slot (BM x BN)
-  const auto rs = sk_rsrc(g.sk_part + (long long)blockIdx.x * SLOT);
+__device__ __forceinline__ void sk_store_piece(const ConvArgs& g, const f32x16 (&acc)[TM][TN], int wave, int lane,
+                                               long long slot) {
+  constexpr int SLOT = NW * TM * TN * 16 * 64;              // floats per slot (BM x BN)
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const auto rs = sk_rsrc(g.sk_part + slot * SLOT);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        typedef int i32x4 __attribute__((ext_vector_type(4)));
         const i32x4 v = {__float_as_int(acc[i][j][4 * q]), __float_as_int(acc[i][j][4 * q + 1]),
                          __float_as_int(acc[i][j][4 * q + 2]), __float_as_int(acc[i][j][4 * q + 3])};
         const int off = (((((wave * TM + i) * TN + j) * 4 + q) * 64) + lane) * 16;
         __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);    // aux 16 = sc1 (write-through)
       }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // every storing wave drains
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store(g.sk_flags + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// acc += the partial of block b (published by sk_publish), after its flag.
-// ONE lane polls ONE word, relaxed, at most g.sk_spins times (~1 s at the
-// default).  Seen: the flag is zeroed again (this block is its only reader)
-// and the partial added.  Not seen: nothing is added, the flag is left alone
-// (its late publisher may still set it) and the library's device error word
-// g.sk_err counts the failure -- jr_device_check() reports it as
-// JR_ERR_DEVICE and re-zeroes every hand-off flag, so a timed-out launch
-// yields an error, never numbers, and never poisons a later launch.
+// acc (= piece k of the tile, or loaded here when `load_first`) += pieces
+// k + 1 .. npieces - 1, in order, from their slots.
 template <int TM, int TN, int NW = 4>
-__device__ __forceinline__ void sk_absorb(const ConvArgs& g, f32x16 (&acc)[TM][TN], int b, int wave, int lane) {
+__device__ __forceinline__ void sk_sum_pieces(const ConvArgs& g, f32x16 (&acc)[TM][TN], int wave, int lane, int owner,
+                                              int npieces, bool load_first) {
   constexpr int SLOT = NW * TM * TN * 16 * 64;
-  __shared__ int s_seen;
-  if (threadIdx.x == 0) {
-    int seen = 0;
-    for (unsigned spins = 0; spins < g.sk_spins; ++spins) {
-      if (__hip_atomic_load(g.sk_flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
-        seen = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below the count)
+  for (int k = load_first ? 0 : 1; k < npieces; ++k) {
+    // the owner's piece sits in its second slot, every later block's in its first
+    const auto rs = sk_rsrc(g.sk_part + (2LL * (owner + k) + (k == 0 ? 1 : 0)) * SLOT);
+    // one accumulator row i at a time (TN x 4 loads in flight): the loaded
+    // piece never holds more than TN x 16 VGPRs
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      i32x4 v[TN][4];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)   // every load of the hand-off sc1 (write-through producers, drained)
+          v[j][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (((((wave * TM + i) * TN + j) * 4 + q) * 64) + lane) * 16,
+                                                          0, 16);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = __int_as_float(v[j][q][e]);
+            acc[i][j][4 * q + e] = k == 0 ? x : acc[i][j][4 * q + e] + x;
+          }
     }
-    if (seen)
-      __hip_atomic_store(g.sk_flags + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      __hip_atomic_fetch_add(g.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_seen = seen;
+  }
+}
+
+constexpr unsigned kSkOwnerBit = 1u << 16;   // low 16 bits: pieces published
+
+template <int TM, int TN, int NW = 4>
+__device__ __forceinline__ bool sk_handoff(const ConvArgs& g, f32x16 (&acc)[TM][TN], int wave, int lane, int owner,
+                                           int npieces, int kind) {
+  __shared__ int s_state;   // 0: move on, 1: finish from registers (+ later pieces), 2: finish loading every piece
+  unsigned* word = g.sk_flags + owner;
+  const unsigned n = (unsigned)npieces;
+  auto bad = [&](unsigned old) { return (old >> 17) != 0 || (old & 0xffffu) >= n; };
+  if (kind == 1) {          // the owner: probe first
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(word, kSkOwnerBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool all = (old & 0xffffu) == n - 1;
+      if (bad(old) || (old & kSkOwnerBit)) __hip_atomic_fetch_add(g.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (all) __hip_atomic_store(word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_state = all ? 1 : 0;
+    }
+    __syncthreads();
+    const int st = s_state;
+    __syncthreads();
+    if (st == 1) {
+      sk_sum_pieces<TM, TN, NW>(g, acc, wave, lane, owner, npieces, false);
+      return true;
+    }
+  }
+  // publish this piece, then count it
+  sk_store_piece<TM, TN, NW>(g, acc, wave, lane, 2LL * blockIdx.x + kind);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = (old & 0xffffu) + 1 == n;
+    if (bad(old)) __hip_atomic_fetch_add(g.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (last) __hip_atomic_store(word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_state = last ? (kind == 1 ? 1 : 2) : 0;
   }
   __syncthreads();
-  const int ok = s_seen;
-  __syncthreads();                     // every wave has read s_seen before the next absorb writes it
-  if (!ok) return;                     // (uniform)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below the poll)
-  const auto rs = sk_rsrc(g.sk_part + (long long)b * SLOT);
-  typedef int i32x4 __attribute__((ext_vector_type(4)));
-  // one accumulator row i at a time (TN x 4 loads in flight): the loaded
-  // partial never holds more than TN x 16 VGPRs
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    i32x4 v[TN][4];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)   // every load of the hand-off sc1 (write-through producer, drained)
-        v[j][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, (((((wave * TM + i) * TN + j) * 4 + q) * 64) + lane) * 16,
-                                                        0, 16);
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += __int_as_float(v[j][q][e]);
-  }
+  const int st = s_state;
+  __syncthreads();          // every wave has read s_state before the next hand-off writes it
+  if (st == 0) return false;                                // (uniform)
+  sk_sum_pieces<TM, TN, NW>(g, acc, wave, lane, owner, npieces, st == 2);
+  return true;
+}
+
+// Where a stream-K segment [kt0, kt1) of `tile` hands off: true if the tile
+// is cut (then owner / npieces / kind for sk_handoff).
+__device__ __forceinline__ bool sk_cut(const ConvArgs& g, int tile, int kt0, int kt1, int* owner, int* npieces,
+                                       int* kind) {
+  if (kt0 == 0 && kt1 == g.ktiles) return false;
+  const long long t0 = (long long)tile * g.ktiles;       // the tile's first iteration
+  *owner = (int)(t0 / g.sk_ipb);
+  *npieces = (int)((t0 + g.ktiles - 1) / g.sk_ipb) - *owner + 1;
+  *kind = kt0 == 0 ? 1 : 0;
+  return true;
 }
 
 

@@ -180,7 +180,7 @@ _SIGS = {
     "jr_stream_wait_event": (c_int, [c_void_p, c_void_p]),
     "jr_event_destroy": (c_int, [c_void_p]),
     "jr_device_check": (c_int, []),
-    "jr_debug_set_sk_spin_limit": (c_int, [ctypes.c_uint32]),
+    "jr_debug_poison_sk_counts": (c_int, [c_void_p, ctypes.c_uint32]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -42,7 +42,7 @@ class EnsembleEngine:
 
     def __init__(self, params: List[np.ndarray], batch: int, height: int = 299, width: int = 299, units: int = 1,
                  device: int | torch.device = 0, dtype: str = "f32", conv_math: Optional[str] = None,
-                 tiles: str = "pinned", head: str = "sigmoid", fuse_pool: Optional[bool] = None, lanes: int = 1):
+                 tiles: str = "pinned", head: str = "sigmoid", fuse_pool: Optional[bool] = None, lanes: int = 2):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if conv_math is None:

@@ -107,9 +107,13 @@ def test_config4_ensemble_vs_fp64(evalset, dtype, grouped):
         assert abs(brier - float(G["brier"])) <= 3 * brier_emu + 2e-4, (brier, brier_emu)
 
 
-def _cli(args, env_extra, cwd):
+def _cli(args, env_extra, cwd, log_dir=None):
     env = dict(os.environ, PYTHONPATH=os.pathsep.join([PKG, ROOT]), **env_extra)
     r = subprocess.run(args, capture_output=True, text=True, env=env, cwd=cwd, timeout=900)
+    if r.returncode != 0 and log_dir is not None:     # the ranks' own stderr (torchrun --redirects)
+        import glob
+        for f in sorted(glob.glob(os.path.join(str(log_dir), "**", "stderr.log"), recursive=True)):
+            print(f"---- {f}\n{open(f).read()[-4000:]}")
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     return r.stdout
 
@@ -127,7 +131,7 @@ def test_cli_two_ranks_equal_one_rank(evalset):
     _cli([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
           "--master-addr", "127.0.0.1", "--master-port", str(port), "--log-dir", str(logs), "--redirects", "3",
           ev, "-o", "--data_dir", data, "-lm", lm, "-so", two_csv, "-b", str(B)],
-         {"JR_DIST_BACKEND": "gloo", "JR_ONE_DEVICE": "1"}, str(d))
+         {"JR_DIST_BACKEND": "gloo", "JR_ONE_DEVICE": "1"}, str(d), log_dir=logs)
     rank0 = list(logs.glob("*/attempt_*/0/stdout.log"))
     assert len(rank0) == 1, rank0
     out2 = rank0[0].read_text()

@@ -259,23 +259,26 @@ def test_stream_k_flags_reset_eager_and_graph():
 
 
 @pytest.mark.parametrize("dtype,cfg", [(X8, SK0 + 11), (BF16, BF_SK0 + 0)])
-def test_stream_k_timeout_is_an_error_not_numbers(dtype, cfg):
-    """VERDICT r04 item 1b/1d, ADVICE r04: an owner block that gives up
-    waiting for a later piece's partial must not add the unpublished slot.
-    With the poll bound lowered to 0 (jr_debug_set_sk_spin_limit: every
-    owner gives up at once) the launch counts its failures into the device
-    error word and jr_device_check raises JR_ERR_DEVICE; the check resets the
-    hand-off flags the late publishers set, so the next launches on the same
-    stream (default bound) are bitwise the clean result again."""
+def test_stream_k_miscount_is_an_error_not_numbers(dtype, cfg):
+    """VERDICT r04 item 1b/1d, ADVICE r04: a stream-K hand-off that goes
+    wrong must raise, never yield numbers.  Blocks no longer wait for one
+    another (the block completing a tile's count finishes it), so the one
+    device-side failure left is a count word not left zero: poisoned here
+    (jr_debug_poison_sk_counts), the launch counts the overrun into the
+    device error word and jr_device_check raises JR_ERR_DEVICE; the check
+    re-zeroes the words, so the next launches on the stream are bitwise the
+    clean result again."""
     ffi = _lib()
     L = ffi.load()
-    n, h, w, cin, cout, kh, kw = 4, 8, 8, 2048, 384, 1, 1     # 30+ pieces per tile: every owner waits
+    n, h, w, cin, cout, kh, kw = 4, 8, 8, 2048, 384, 1, 1     # 30+ pieces per tile
     d = ffi.ConvDesc(n, h, w, cin, cout, kh, kw, 1, 1, 0, 0, h, w, 0, cin, 0, cout)
     g = torch.Generator(device="cuda").manual_seed(11)
     tdt = torch.bfloat16 if dtype == BF16 else torch.float32
     X = torch.randn(n * h * w * cin, device="cuda", generator=g).to(tdt)
     W = (torch.randn(kh * kw * cin * cout, device="cuda", generator=g) * 0.02).to(tdt)
     ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, dtype, 0, cfg))
+    st_ = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st_.cuda_stream)
     try:
         wsb = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, dtype)
         ws = torch.zeros(wsb // 4 + 4, device="cuda")
@@ -284,28 +287,70 @@ def test_stream_k_timeout_is_an_error_not_numbers(dtype, cfg):
         def fwd(Y):
             ffi.check("fwd", L.jr_conv2d_fwd_bn_stats(ctypes.byref(d), dtype, X.data_ptr(), W.data_ptr(),
                                                       Y.data_ptr(), 1e-3, st.data_ptr(), st.data_ptr() + 4 * cout,
-                                                      ws.data_ptr(), wsb, None))
+                                                      ws.data_ptr(), wsb, sp))
+        torch.cuda.synchronize()
         ref = torch.zeros(n * h * w * cout, device="cuda", dtype=tdt)
         fwd(ref)
-        torch.cuda.synchronize()
+        st_.synchronize()
         ffi.device_check()                        # a clean launch reports nothing
-        ffi.check("spin", L.jr_debug_set_sk_spin_limit(0))
-        try:
-            Y = torch.zeros_like(ref)
-            fwd(Y)
-            torch.cuda.synchronize()
-        finally:
-            ffi.check("spin", L.jr_debug_set_sk_spin_limit(1 << 22))
+        ffi.check("poison", L.jr_debug_poison_sk_counts(sp, 1 << 20))
+        Y = torch.zeros_like(ref)
+        fwd(Y)
+        st_.synchronize()
         with pytest.raises(ffi.JRError) as ei:
             ffi.device_check()
         assert ei.value.status == ffi.JR_ERR_DEVICE and "stream-K" in str(ei.value)
         ffi.device_check()                        # reported once, then clear
-        for _ in range(3):                        # the flags were reset: later launches are clean
+        for _ in range(3):                        # the words were reset: later launches are clean
             Y = torch.zeros_like(ref)
             fwd(Y)
-            torch.cuda.synchronize()
+            st_.synchronize()
             assert torch.equal(Y, ref)
         ffi.device_check()
+        assert float(ref.float().abs().max()) > 0
+    finally:
+        ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, dtype, 0, -1))
+
+
+@pytest.mark.parametrize("dtype,cfg", [(X8, SK0 + 11), (BF16, BF_SK0 + 0)])
+def test_stream_k_concurrent_grids_never_stall(dtype, cfg):
+    """Four stream-K grids at once on four streams (each sized to fill the
+    chip alone, so their blocks cannot all be resident together), repeated:
+    with round 4's waiting owners this could stall until the poll bound (the
+    2-rank one-device eval did); the counting hand-off never waits -- every
+    output is bitwise the single-stream result and no failure is counted."""
+    ffi = _lib()
+    L = ffi.load()
+    n, h, w, cin, cout, kh, kw = 16, 17, 17, 768, 384, 1, 1
+    d = ffi.ConvDesc(n, h, w, cin, cout, kh, kw, 1, 1, 0, 0, h, w, 0, cin, 0, cout)
+    g = torch.Generator(device="cuda").manual_seed(12)
+    tdt = torch.bfloat16 if dtype == BF16 else torch.float32
+    X = torch.randn(n * h * w * cin, device="cuda", generator=g).to(tdt)
+    W = (torch.randn(kh * kw * cin * cout, device="cuda", generator=g) * 0.02).to(tdt)
+    ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, dtype, 0, cfg))
+    try:
+        wsb = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, dtype)
+        streams = [torch.cuda.Stream() for _ in range(4)]
+        wss = [torch.zeros(wsb // 4 + 4, device="cuda") for _ in streams]
+        M = n * h * w
+
+        def fwd(Y, k):
+            ffi.check("fwd", L.jr_conv2d_fwd(ctypes.byref(d), dtype, X.data_ptr(), W.data_ptr(), Y.data_ptr(),
+                                             wss[k].data_ptr(), wsb, ctypes.c_void_p(streams[k].cuda_stream)))
+        ref = torch.zeros(M * cout, device="cuda", dtype=tdt)
+        torch.cuda.synchronize()
+        fwd(ref, 0)
+        torch.cuda.synchronize()
+        outs = [[torch.zeros_like(ref) for _ in range(6)] for _ in streams]
+        torch.cuda.synchronize()
+        for r in range(6):
+            for k in range(len(streams)):
+                fwd(outs[k][r], k)
+        torch.cuda.synchronize()
+        ffi.device_check()
+        for k in range(len(streams)):
+            for r in range(6):
+                assert torch.equal(outs[k][r], ref), (k, r)
         assert float(ref.float().abs().max()) > 0
     finally:
         ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, dtype, 0, -1))
