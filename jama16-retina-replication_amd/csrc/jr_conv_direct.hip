@@ -186,8 +186,11 @@ bool conv1_direct_ok(const jr_conv_desc* d, int dtype) {
     const char* e = std::getenv("JR_CONV1_DIRECT");
     return !(e && e[0] == '0');
   }();
-  const int q = dtype == JR_BF16 ? 8 : 4;
-  return on && (dtype == JR_F32 || dtype == JR_F32_X8 || dtype == JR_BF16) && d->c_in <= 3 &&
+  // fp32 only: per kernel (rocprofv3, tools/conv1_probe.py, profiles/r05_conv1_kernels.txt)
+  // the x8 GEMM takes 121 us and this kernel 108 us, but the bf16 GEMM 68.5
+  // us and this kernel 91-103 us -- bf16 keeps the GEMM
+  const int q = 4;
+  return on && (dtype == JR_F32 || dtype == JR_F32_X8) && d->c_in <= 3 &&
          d->x_c_stride == q && d->x_c_off == 0 && d->c_out == kD1Cout && d->y_c_off == 0 &&
          d->y_c_stride == kD1Cout && d->kh == 3 && d->kw == 3 && d->stride_h == 2 && d->stride_w == 2 &&
          d->pad_h == 0 && d->pad_w == 0;

@@ -215,17 +215,31 @@ __device__ __forceinline__ void sk_store_piece(const ConvArgs& g, const f32x16 (
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // every storing wave drains
 }
 
-// acc (= piece k of the tile, or loaded here when `load_first`) += pieces
-// k + 1 .. npieces - 1, in order, from their slots.
+// acc (= the owner's piece, in registers) += pieces 1 .. npieces - 1, in
+// order, from their slots; load_first: acc is first set to the owner's piece
+// from its slot (a later block finishing the tile).
 template <int TM, int TN, int NW = 4>
 __device__ __forceinline__ void sk_sum_pieces(const ConvArgs& g, f32x16 (&acc)[TM][TN], int wave, int lane, int owner,
                                               int npieces, bool load_first) {
   constexpr int SLOT = NW * TM * TN * 16 * 64;
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below the count)
-  for (int k = load_first ? 0 : 1; k < npieces; ++k) {
-    // the owner's piece sits in its second slot, every later block's in its first
-    const auto rs = sk_rsrc(g.sk_part + (2LL * (owner + k) + (k == 0 ? 1 : 0)) * SLOT);
+  if (load_first) {   // the owner's piece sits in its second slot
+    const auto rs = sk_rsrc(g.sk_part + (2LL * owner + 1) * SLOT);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (((((wave * TM + i) * TN + j) * 4 + q) * 64) + lane) * 16,
+                                                                0, 16);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] = __int_as_float(v[e]);
+        }
+  }
+  for (int k = 1; k < npieces; ++k) {   // every later block's piece sits in its first slot
+    const auto rs = sk_rsrc(g.sk_part + 2LL * (owner + k) * SLOT);
     // one accumulator row i at a time (TN x 4 loads in flight): the loaded
     // piece never holds more than TN x 16 VGPRs
 #pragma unroll
@@ -242,10 +256,7 @@ __device__ __forceinline__ void sk_sum_pieces(const ConvArgs& g, f32x16 (&acc)[T
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float x = __int_as_float(v[j][q][e]);
-            acc[i][j][4 * q + e] = k == 0 ? x : acc[i][j][4 * q + e] + x;
-          }
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += __int_as_float(v[j][q][e]);
     }
   }
 }
@@ -255,41 +266,41 @@ constexpr unsigned kSkOwnerBit = 1u << 16;   // low 16 bits: pieces published
 template <int TM, int TN, int NW = 4>
 __device__ __forceinline__ bool sk_handoff(const ConvArgs& g, f32x16 (&acc)[TM][TN], int wave, int lane, int owner,
                                            int npieces, int kind) {
-  __shared__ int s_state;   // 0: move on, 1: finish from registers (+ later pieces), 2: finish loading every piece
+  // s_state: 0 move on, 1 finish with the owner's piece in registers, 2 finish loading every piece
+  __shared__ int s_state;
   unsigned* word = g.sk_flags + owner;
   const unsigned n = (unsigned)npieces;
-  auto bad = [&](unsigned old) { return (old >> 17) != 0 || (old & 0xffffu) >= n; };
+  int st = 0;
   if (kind == 1) {          // the owner: probe first
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned old = __hip_atomic_fetch_add(word, kSkOwnerBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool all = (old & 0xffffu) == n - 1;
-      if (bad(old) || (old & kSkOwnerBit)) __hip_atomic_fetch_add(g.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((old >> 16) != 0 || (old & 0xffffu) >= n)
+        __hip_atomic_fetch_add(g.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (all) __hip_atomic_store(word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_state = all ? 1 : 0;
     }
     __syncthreads();
-    const int st = s_state;
+    st = s_state;
     __syncthreads();
-    if (st == 1) {
-      sk_sum_pieces<TM, TN, NW>(g, acc, wave, lane, owner, npieces, false);
-      return true;
+  }
+  if (st == 0) {            // publish this piece, then count it
+    sk_store_piece<TM, TN, NW>(g, acc, wave, lane, 2LL * blockIdx.x + kind);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = (old & 0xffffu) + 1 == n;
+      if ((old >> 17) != 0 || (old & 0xffffu) >= n)
+        __hip_atomic_fetch_add(g.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (last) __hip_atomic_store(word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_state = last ? (kind == 1 ? 1 : 2) : 0;
     }
+    __syncthreads();
+    st = s_state;
+    __syncthreads();        // every wave has read s_state before the next hand-off writes it
+    if (st == 0) return false;                              // (uniform)
   }
-  // publish this piece, then count it
-  sk_store_piece<TM, TN, NW>(g, acc, wave, lane, 2LL * blockIdx.x + kind);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = (old & 0xffffu) + 1 == n;
-    if (bad(old)) __hip_atomic_fetch_add(g.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (last) __hip_atomic_store(word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_state = last ? (kind == 1 ? 1 : 2) : 0;
-  }
-  __syncthreads();
-  const int st = s_state;
-  __syncthreads();          // every wave has read s_state before the next hand-off writes it
-  if (st == 0) return false;                                // (uniform)
   sk_sum_pieces<TM, TN, NW>(g, acc, wave, lane, owner, npieces, st == 2);
   return true;
 }
