@@ -28,3 +28,10 @@ print("by (consumer phase, producer phase):", dict(cnt))
 cnt = Counter((c.name, p.name, phase[c.idx], phase[p.idx]) for c, p in pw)
 for k, v in cnt.most_common(30):
     print(f"  {v:4d}  {k[0]:18s} <- {k[1]:18s} ({k[2]} <- {k[3]})")
+if "-v" in sys.argv:
+    for c in seq:
+        def why(c, p):
+            r = (set(c.reads) | set(c.writes)) & set(p.writes) | (set(c.writes) & set(p.reads))
+            return "/".join(str(k) for k in sorted(r, key=str))[:60]
+        w = ",".join(f"{seq[j].name}@{lj}#{j}[{why(c, seq[j])}]" for lj, j in c.pwaits)
+        print(f"{c.idx:4d} L{c.lane} {phase[c.idx]} {c.name:18s} {'REC' if c.record else '   '} {('<- ' + w) if w else ''}")
