@@ -177,7 +177,7 @@ def pmc_traffic(dtype: str, B: int, res: int, math: str = "x8") -> dict:
     if (B, res) != (64, 299):
         return {}
     tag = {"f32": "f32mfma", "x8p": "f32x8p"}.get(math, "f32") if dtype == "f32" else dtype
-    for rnd in ("r04", "r03", "r02c", "r02", "r01"):      # the newest committed summary of this workload
+    for rnd in ("r05", "r04", "r03", "r02c", "r02", "r01"):      # the newest committed summary of this workload
         p = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{tag}.json")
         if os.path.exists(p):
             break
