@@ -284,8 +284,10 @@ def max_over_ranks(dist, v: float) -> float:
 def grouped_conv_roofline(ens, steps: int = 3):
     """The conv roofline of the grouped ensemble forward (BASELINE config 4):
     HIP events (on the stream each call is enqueued on) bracket every grouped
-    conv + statistics launch of one lane-0 pass; algorithmic FLOPs = members x
-    batch x 2 x MACs per image."""
+    conv + statistics launch, each run alone (the device synchronised before
+    and after it: with two lanes a neighbour launch would share the CUs and
+    inflate its time); algorithmic FLOPs = members x batch x 2 x MACs per
+    image."""
     from jr import _ffi
     calls, _ = ens._build_calls(ens.batch)
     flops = sum(2 * n.macs_per_image() for n in ens.g.convs) * ens.batch * ens.members
@@ -295,9 +297,11 @@ def grouped_conv_roofline(ens, steps: int = 3):
             st = ens.lane_streams[c.lane]
             if c.name == "conv_fwd":
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
                 e0.record(st)
                 rc = c.fn(*c.args)
                 e1.record(st)
+                torch.cuda.synchronize()
                 pairs.append((e0, e1))
             else:
                 rc = c.fn(*c.args)
