@@ -270,6 +270,26 @@ typedef struct jr_bn_seg {
 int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
                          int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd, void* dx,
                          void* ws, size_t ws_bytes, void* stream);
+/* Up to 8 independent conv2d_bn backwards (the branch-final layers of one
+ * Inception block, whose upstream gradients become final together) in ONE
+ * set of three launches; layer l is exactly the jr_bn_relu_bwd_multi call
+ * with its fields (bitwise the same results), each with at most 512 reduce
+ * chunks (the 35^2 / 17^2 / 8^2 shapes at batch 64; larger ones:
+ * JR_ERR_UNSUPPORTED).  ws: jr_bn_relu_bwd_batch_workspace_size bytes. */
+typedef struct jr_bn_bwd_layer {
+  int32_t nseg;
+  jr_bn_seg segs[4];
+  const void* x;
+  int32_t x_c_off, x_c_stride;
+  int64_t m;
+  int32_t c;
+  const float* mean;
+  const float* invstd;
+  void* dx;
+} jr_bn_bwd_layer;
+size_t jr_bn_relu_bwd_batch_workspace_size(int32_t n, const jr_bn_bwd_layer* layers);
+int jr_bn_relu_bwd_batch(int dtype, int32_t n, const jr_bn_bwd_layer* layers, void* ws, size_t ws_bytes,
+                         void* stream);
 /* The backward of a conv2d_bn layer whose output only a 3x3/2 max-pool reads
  * (forward: jr_bn_relu_maxpool3x3s2_fwd): the max-pool backward writes dy
  * (d's x slice, from the pooled gradient at d's y slice and the argmax) and

@@ -166,11 +166,12 @@ __device__ __forceinline__ int seg_of(const BnSegs& sg, int ch) {
 // per row and operand) until used, so red_rows<MODE>() rows are in flight
 // per thread: the loop is latency-bound, not bandwidth-bound, with fewer.
 // Partials: part[2][c][nchunks] (fp64, chunk-contiguous for the finalize).
+// (body: chunk bx of nch; k_bn_reduce runs chunk blockIdx.x of gridDim.x,
+// k_bn_reduce_batch a layer's chunk of a batched launch)
 template <int MODE, typename T>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
-k_bn_reduce(const T* __restrict__ x, int xs, BnSegs sg, int64_t m, int c,
-                                                   int rows_per_chunk, const float* __restrict__ mean,
-                                                   const float* __restrict__ invstd, double* part) {
+__device__ __forceinline__ void bn_reduce_body(const T* __restrict__ x, int xs, const BnSegs& sg, int64_t m, int c,
+                                               int rows_per_chunk, const float* __restrict__ mean,
+                                               const float* __restrict__ invstd, double* part, int bx, int64_t nch) {
   constexpr int VW = Vec<T>::N;
   constexpr int U = red_rows<MODE>();
   __shared__ double red[256 * 2 * VW];
@@ -178,7 +179,7 @@ k_bn_reduce(const T* __restrict__ x, int xs, BnSegs sg, int64_t m, int c,
   const int rpp = 256 / tpr;
   const int t = threadIdx.x;
   const int q = t % tpr, rr = t / tpr;
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
+  const int64_t r0 = (int64_t)bx * rows_per_chunk;
   const int64_t r1 = min(m, r0 + rows_per_chunk);
   double s0[VW], s1[VW];
 #pragma unroll
@@ -292,13 +293,19 @@ k_bn_reduce(const T* __restrict__ x, int xs, BnSegs sg, int64_t m, int c,
     __syncthreads();
   }
   if (t < tpr) {
-    const int64_t nch = gridDim.x;
 #pragma unroll
     for (int j = 0; j < VW; ++j) {
-      part[(int64_t)(q * VW + j) * nch + blockIdx.x] = red[t * 2 * VW + j];
-      part[(int64_t)(c + q * VW + j) * nch + blockIdx.x] = red[t * 2 * VW + VW + j];
+      part[(int64_t)(q * VW + j) * nch + bx] = red[t * 2 * VW + j];
+      part[(int64_t)(c + q * VW + j) * nch + bx] = red[t * 2 * VW + VW + j];
     }
   }
+}
+
+template <int MODE, typename T>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2)))
+k_bn_reduce(const T* __restrict__ x, int xs, BnSegs sg, int64_t m, int c, int rows_per_chunk,
+            const float* __restrict__ mean, const float* __restrict__ invstd, double* part) {
+  bn_reduce_body<MODE, T>(x, xs, sg, m, c, rows_per_chunk, mean, invstd, part, blockIdx.x, gridDim.x);
 }
 
 // Fixed-order combine of the chunk partials: one wave per channel; lane j
@@ -468,11 +475,10 @@ __global__ void __launch_bounds__(256) k_bn_relu_apply_stats(const T* __restrict
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(BnSegs sg, const T* __restrict__ x, int xs, int64_t m,
-                                                           int c, const float* __restrict__ mean,
-                                                           const float* __restrict__ invstd,
-                                                           const float* __restrict__ k1,
-                                                           const float* __restrict__ k2, T* dx) {
+__device__ __forceinline__ void bn_bwd_apply_body(const BnSegs& sg, const T* __restrict__ x, int xs, int64_t m, int c,
+                                                  const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                  const float* __restrict__ k1, const float* __restrict__ k2, T* dx,
+                                                  int bx) {
   constexpr int VW = Vec<T>::N;
   const int tpr = c / VW;
   const int rpp = 256 / tpr;
@@ -488,7 +494,7 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(BnSegs sg, const T* _
     const int k = q * VW + j;
     mu[j] = mean[k]; is[j] = invstd[k]; be[j] = sg.beta[sgi][lc + j]; c1[j] = k1[k]; c2[j] = k2[k];
   }
-  const int64_t r0 = (int64_t)blockIdx.x * rpp * kAppUnroll + rr;
+  const int64_t r0 = (int64_t)bx * rpp * kAppUnroll + rr;
   // unconditional loads (rows past m re-read row m - 1), unpacked after all
   // were issued (as in k_bn_relu_apply)
   uint4 xr[kAppUnroll], gr[kAppUnroll];
@@ -519,6 +525,15 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(BnSegs sg, const T* _
     }
     Vec<T>::st(dx + r * xs + q * VW, o);
   }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(BnSegs sg, const T* __restrict__ x, int xs, int64_t m,
+                                                           int c, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ k1,
+                                                           const float* __restrict__ k2, T* dx) {
+  bn_bwd_apply_body<T>(sg, x, xs, m, c, mean, invstd, k1, k2, dx, blockIdx.x);
 }
 
 // Canonical combine of ONE channel's backward-reduce partials when there are
@@ -555,9 +570,9 @@ __device__ __forceinline__ void bwd_combine8(const double* __restrict__ p0, cons
 }
 
 // k_bn_finalize<1> for at most kFoldMaxP chunks: 32 channels per block.
-__global__ void __launch_bounds__(256) k_bn_finalize8(const double* __restrict__ part, int nchunks, int c, int64_t m,
-                                                      float* k1, float* k2, BnSegs sg) {
-  const int k = blockIdx.x * (256 / kStatsLanes) + threadIdx.x / kStatsLanes, j = threadIdx.x % kStatsLanes;
+__device__ __forceinline__ void bn_finalize8_body(const double* __restrict__ part, int nchunks, int c, int64_t m,
+                                                  float* k1, float* k2, const BnSegs& sg, int bx) {
+  const int k = bx * (256 / kStatsLanes) + threadIdx.x / kStatsLanes, j = threadIdx.x % kStatsLanes;
   if (k >= c) return;   // (whole 8-lane groups)
   double s0, s1;
   bwd_combine8(part + (int64_t)k * nchunks, part + (int64_t)(c + k) * nchunks, nchunks, j, &s0, &s1);
@@ -567,6 +582,11 @@ __global__ void __launch_bounds__(256) k_bn_finalize8(const double* __restrict__
   k2[k] = (float)(s1 * inv_m);
   const int sgi = seg_of(sg, k);
   sg.dbeta[sgi][k - sg.c0[sgi]] = (float)s0;
+}
+
+__global__ void __launch_bounds__(256) k_bn_finalize8(const double* __restrict__ part, int nchunks, int c, int64_t m,
+                                                      float* k1, float* k2, BnSegs sg) {
+  bn_finalize8_body(part, nchunks, c, m, k1, k2, sg, blockIdx.x);
 }
 
 // The backward's finalize folded into its apply: block (bx, by) combines the
@@ -647,6 +667,58 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply_fold(BnSegs sg, const
       Vec<T>::st(dx + r * xs + ch, o);
     }
   }
+}
+
+// Several independent layers' backwards in ONE set of three launches
+// (jr_bn_relu_bwd_batch): layer l owns blocks [b0, b0 + blocks) of each
+// launch and runs exactly the single-layer bodies on them (same chunk
+// geometry, same finalize arithmetic: bitwise jr_bn_relu_bwd_multi per layer).
+constexpr int kBnBatchMax = 8;
+struct BnBatchLayer {
+  BnSegs sg;
+  const void* x;
+  void* dx;
+  const float* mean;
+  const float* invstd;
+  double* part;
+  float* k1;
+  float* k2;
+  int64_t m;
+  int c, xs, rpc, nchunks;
+  int b0[3];   // first block in the reduce / finalize / apply launch
+};
+struct BnBatch {
+  BnBatchLayer L[kBnBatchMax];
+  int n;
+};
+
+// the layer owning block b of launch `which` (wave-uniform linear scan)
+__device__ __forceinline__ int bn_batch_layer(const BnBatch& bt, int which, int b) {
+  int l = 0;
+  for (int i = 1; i < bt.n; ++i) l = b >= bt.L[i].b0[which] ? i : l;
+  return l;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) k_bn_reduce_batch(BnBatch bt) {
+  const int l = bn_batch_layer(bt, 0, blockIdx.x);
+  const BnBatchLayer& L = bt.L[l];
+  bn_reduce_body<1, T>(static_cast<const T*>(L.x), L.xs, L.sg, L.m, L.c, L.rpc, L.mean, L.invstd, L.part,
+                       blockIdx.x - L.b0[0], L.nchunks);
+}
+
+__global__ void __launch_bounds__(256) k_bn_finalize8_batch(BnBatch bt) {
+  const int l = bn_batch_layer(bt, 1, blockIdx.x);
+  const BnBatchLayer& L = bt.L[l];
+  bn_finalize8_body(L.part, L.nchunks, L.c, L.m, L.k1, L.k2, L.sg, blockIdx.x - L.b0[1]);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_relu_bwd_apply_batch(BnBatch bt) {
+  const int l = bn_batch_layer(bt, 2, blockIdx.x);
+  const BnBatchLayer& L = bt.L[l];
+  bn_bwd_apply_body<T>(L.sg, static_cast<const T*>(L.x), L.xs, L.m, L.c, L.mean, L.invstd, L.k1, L.k2,
+                       static_cast<T*>(L.dx), blockIdx.x - L.b0[2]);
 }
 
 static int apply_grid(int64_t m, int c, int vw) {
@@ -895,6 +967,74 @@ JR_API int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, cons
   const int rc = bwd_setup(dtype, nseg, segs, x, x_c_off, x_c_stride, m, c, mean, invstd, dx, sg);
   if (rc) return rc;
   return bn_bwd_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, dx, ws, ws_bytes, as_stream(stream));
+}
+
+// workspace of a batched backward: each layer's ws_need, 256-byte aligned
+static size_t batch_ws(int n, const jr_bn_bwd_layer* layers) {
+  size_t off = 0;
+  for (int l = 0; l < n; ++l) off += (ws_need(layers[l].m, layers[l].c) + 255) / 256 * 256;
+  return off;
+}
+
+JR_API size_t jr_bn_relu_bwd_batch_workspace_size(int32_t n, const jr_bn_bwd_layer* layers) {
+  if (n < 1 || n > kBnBatchMax || !layers) return 0;
+  return batch_ws(n, layers);
+}
+
+JR_API int jr_bn_relu_bwd_batch(int dtype, int32_t n, const jr_bn_bwd_layer* layers, void* ws, size_t ws_bytes,
+                                void* stream) {
+  if (n < 1 || n > kBnBatchMax || !layers) return fail(JR_ERR_INVALID, "bn_relu_bwd_batch: 1..8 layers");
+  if (!ws || ws_bytes < batch_ws(n, layers)) return fail(JR_ERR_WORKSPACE, "bn_relu_bwd_batch: workspace too small");
+  const int vw = vec_width(dtype);
+  BnBatch bt{};
+  bt.n = n;
+  int blocks[3] = {0, 0, 0};
+  size_t off = 0;
+  for (int l = 0; l < n; ++l) {
+    const jr_bn_bwd_layer& e = layers[l];
+    BnBatchLayer& L = bt.L[l];
+    const void* x = e.x;
+    void* dx = e.dx;
+    const int rc = bwd_setup(dtype, e.nseg, e.segs, x, e.x_c_off, e.x_c_stride, e.m, e.c, e.mean, e.invstd, dx, L.sg);
+    if (rc) return rc;
+    const ChunkGeom g = chunk_geom(e.m, e.c, vw);
+    if (g.nchunks > kFoldMaxP)
+      return fail(JR_ERR_UNSUPPORTED, "bn_relu_bwd_batch: a layer with more than 512 reduce chunks (use jr_bn_relu_bwd_multi)");
+    L.x = x;
+    L.dx = dx;
+    L.mean = e.mean;
+    L.invstd = e.invstd;
+    L.part = reinterpret_cast<double*>(static_cast<char*>(ws) + off);
+    L.k1 = reinterpret_cast<float*>(L.part + (size_t)g.nchunks * 2 * e.c);
+    L.k2 = L.k1 + e.c;
+    L.m = e.m;
+    L.c = e.c;
+    L.xs = e.x_c_stride;
+    L.rpc = g.rows_per_chunk;
+    L.nchunks = g.nchunks;
+    L.b0[0] = blocks[0];
+    L.b0[1] = blocks[1];
+    L.b0[2] = blocks[2];
+    blocks[0] += g.nchunks;
+    blocks[1] += (int)ceil_div(e.c, kFoldCh);
+    blocks[2] += apply_grid(e.m, e.c, vw);
+    off += (ws_need(e.m, e.c) + 255) / 256 * 256;
+  }
+  hipStream_t s = as_stream(stream);
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_bn_reduce_batch<float>, dim3(blocks[0]), dim3(256), 0, s, bt);
+  else
+    hipLaunchKernelGGL(k_bn_reduce_batch<uint16_t>, dim3(blocks[0]), dim3(256), 0, s, bt);
+  int rc = check_launch("bn_bwd batch reduce");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_bn_finalize8_batch, dim3(blocks[1]), dim3(256), 0, s, bt);
+  rc = check_launch("bn_bwd batch finalize");
+  if (rc) return rc;
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_bn_relu_bwd_apply_batch<float>, dim3(blocks[2]), dim3(256), 0, s, bt);
+  else
+    hipLaunchKernelGGL(k_bn_relu_bwd_apply_batch<uint16_t>, dim3(blocks[2]), dim3(256), 0, s, bt);
+  return check_launch("bn_bwd batch apply");
 }
 
 // ---------------------------------------------------------------------------

@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("JR_LIB", os.path.join(_HERE, "libjr.so"))
 
 JR_OK = 0
+JR_ERR_INVALID, JR_ERR_HIP, JR_ERR_UNSUPPORTED, JR_ERR_WORKSPACE = -1, -2, -3, -4   # include/jr.h jr_status
 JR_ERR_DEVICE = -5   # jr_device_check: a kernel reported a device-side failure
 JR_F32 = 0
 JR_BF16 = 1
@@ -49,6 +50,13 @@ class BnSeg(Structure):
     """include/jr.h jr_bn_seg: one member's upstream gradient slice and beta / dbeta."""
     _fields_ = [("dy", c_void_p), ("dy_c_off", c_int32), ("dy_c_stride", c_int32), ("c", c_int32),
                 ("beta", c_void_p), ("dbeta", c_void_p)]
+
+
+class BnBwdLayer(Structure):
+    """include/jr.h jr_bn_bwd_layer: one layer of a batched BN backward."""
+    _fields_ = [("nseg", c_int32), ("segs", BnSeg * 4), ("x", c_void_p), ("x_c_off", c_int32),
+                ("x_c_stride", c_int32), ("m", c_int64), ("c", c_int32), ("mean", c_void_p),
+                ("invstd", c_void_p), ("dx", c_void_p)]
 
 
 class WgradSeg(Structure):
@@ -121,6 +129,8 @@ _SIGS = {
     "jr_comm_world": (c_int, [c_void_p]),
     "jr_comm_destroy": (c_int, [c_void_p]),
     "jr_bn_workspace_size": (c_size_t, [c_int64, c_int32]),
+    "jr_bn_relu_bwd_batch_workspace_size": (c_size_t, [c_int32, c_void_p]),
+    "jr_bn_relu_bwd_batch": (c_int, [c_int, c_int32, c_void_p, c_void_p, c_size_t, c_void_p]),
     "jr_bn_stats": (c_int, [c_int, c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
                             c_void_p, c_size_t, c_void_p]),
     "jr_bn_relu_apply": (c_int, [c_int, c_void_p, c_int32, c_int32, c_int64, c_int32, c_void_p, c_void_p,

@@ -268,6 +268,17 @@ class Engine:
                                if self.nlanes > 1 and not self.x8p else None)
             self.draw = self.draw_lane[0]
             self.dfeat = self._t(B * feat_c)
+            # the block-output BN backwards batched per block (jr_bn_relu_bwd_batch,
+            # opt-in JR_BN_BATCH=1: bitwise the per-layer launch sets, measured
+            # neutral -- bf16 9.343 -> 9.359, f32 24.85 -> 24.90 ms, the per-layer
+            # sets already overlap on the two lanes): their raw gradients live in
+            # two alternating sets of per-layer buffers
+            self.bn_batch = (self._bn_batch_groups(B)
+                             if not self.x8p and os.environ.get("JR_BN_BATCH", "0") == "1" else [])
+            slots = max((len(grp) for grp in self.bn_batch), default=0)
+            self.drawb = [[self._t(max(B * grp[k].ho * grp[k].wo * grp[k].cout
+                                       for grp in self.bn_batch if k < len(grp)), at) for k in range(slots)]
+                          for _ in range(2 if slots else 0)]
         if self.dt == _ffi.JR_BF16 or self.x8p:
             self._alloc_bf16_filters(planes=3 if self.x8p else 1)
         if self.x8p:
@@ -279,6 +290,9 @@ class Engine:
             for op in (ops if self.train_mode else ops[:1]):
                 ws = max(ws, self.lib.jr_conv2d_workspace_size(ctypes.byref(d), op, self.cdt))
             ws = max(ws, self.lib.jr_bn_workspace_size(B * u.ho * u.wo, u.cout))   # one backward per launch (or less)
+        for grp in getattr(self, "bn_batch", []):        # one batched BN backward per block
+            ws = max(ws, sum((self.lib.jr_bn_workspace_size(B * u.ho * u.wo, u.cout) + 255) // 256 * 256
+                             for u in grp))
         for i in self.pool_fused:                      # the fused max-pool + BN backward's partials
             ws = max(ws, self.lib.jr_bn_relu_bwd_maxpool_workspace_size(ctypes.byref(self._pool_desc(g.nodes[i], B))))
         self.ws_bytes = int(ws)
@@ -287,6 +301,38 @@ class Engine:
         self.ws_stem = (self._t((self.ws_bytes + 15) // 4 + 4)
                         if self.train_mode and getattr(self, "draw_stem2", None) is not None else None)
         self.ws = self.ws_lane[0]
+
+    def _bn_batch_groups(self, B: int):
+        """Conv launches whose BN backwards become due together: every member
+        writes a slice of one block buffer (several producing launches: the
+        branch-final layers of an Inception block), one launch set per launch
+        (c / vector width <= 256), at most 512 reduce chunks (jr_bn.hip
+        chunk_geom), not the stem's pooled layers; blocks with two or more."""
+        g, vw = self.g, (8 if self.dt == _ffi.JR_BF16 else 4)
+        producers: Dict[int, set] = {}
+        for u in self.cunits:
+            for m in u.members:
+                producers.setdefault(m.y.buf, set()).add(u.first.idx)
+        for n in g.nodes:
+            if n.kind != "conv":
+                producers.setdefault(n.y.buf, set()).add(("pool", id(n)))
+        fused = set(self.pool_fused.values())
+        groups: Dict[int, list] = {}
+        for u in self.cunits:
+            bufs = {m.y.buf for m in u.members}
+            if len(bufs) != 1:
+                continue
+            buf = next(iter(bufs))
+            M, c = B * u.ho * u.wo, u.cout
+            tpr = c // vw
+            rpp = max(1, 256 // tpr)
+            step = rpp * 16
+            rpc = -(-max(-(-M // 1024), step) // step) * step
+            if (len(producers[buf]) < 2 or buf in fused or buf == g.output_buf or tpr > 256
+                    or -(-M // rpc) > 512):
+                continue
+            groups.setdefault(buf, []).append(u)
+        return [grp for grp in groups.values() if len(grp) >= 2]
 
     def _alloc_planes(self) -> None:
         """JR_F32_X8P operand planes (jr.h): the exact bf16 h/m/l split of
@@ -736,6 +782,12 @@ class Engine:
             stem_split = (nl > 1 and self.draw_stem2 is not None
                           and os.environ.get("JR_STEM_WGRAD_LANE", "1") != "0")
             sbuf = 0
+            # batched block-output BN backwards: unit -> (group, slot); a group
+            # is issued where its first unit comes up (its upstream gradients
+            # are final there), on that unit's lane, into set `bset`
+            in_batch = {u.first.idx: (gi, k) for gi, grp in enumerate(self.bn_batch) for k, u in enumerate(grp)}
+            batch_draw: Dict[int, Tuple[int, Tuple]] = {}   # uid -> (raw-gradient pointer, resource)
+            bset = 0
             for i in range(len(g.nodes) - 1, -1, -1):
                 n = g.nodes[i]
                 ln = lane_of[i]
@@ -758,6 +810,35 @@ class Engine:
                             draw, dkey = self.draw_stem2.data_ptr(), ("draw2", 0)
                         sbuf ^= 1
                         wl = 1
+                    if uid in in_batch and uid not in batch_draw:   # the block's batched BN backward
+                        grp = self.bn_batch[in_batch[uid][0]]
+                        layers = (_ffi.BnBwdLayer * len(grp))()
+                        reads, writes = [("r", v.first.idx) for v in grp] + [("p",)], [("ws", ln)]
+                        for k, v in enumerate(grp):
+                            vid = v.first.idx
+                            ptr = self.drawb[bset][k].data_ptr()
+                            batch_draw[vid] = (ptr, ("drawb", bset, k))
+                            segs = [_ffi.BnSeg(D(m.y.buf), m.y.c_off, g.bufs[m.y.buf].c, m.cout,
+                                               self._p(f"batch_normalization_{m.idx + 1}/beta"),
+                                               self._gp(f"batch_normalization_{m.idx + 1}/beta")) for m in v.members]
+                            layers[k].nseg = len(segs)
+                            for j, sgm in enumerate(segs):
+                                layers[k].segs[j] = sgm
+                            layers[k].x = self.raw_unit[vid].data_ptr()
+                            layers[k].x_c_off, layers[k].x_c_stride = 0, v.cout
+                            layers[k].m, layers[k].c = B * v.ho * v.wo, v.cout
+                            layers[k].mean = self.mean_unit[vid].data_ptr()
+                            layers[k].invstd = self.invstd_unit[vid].data_ptr()
+                            layers[k].dx = ptr
+                            reads += [("d", m.y.buf, m.y.c_off) for m in v.members]
+                            writes += [("drawb", bset, k), ("g", vid)]
+                        keep.append(layers)
+                        add(bwd, L.jr_bn_relu_bwd_batch, (dt, len(grp), ctypes.byref(layers), ws, wsb, s),
+                            "bn_relu_bwd", ln, reads, writes,
+                            nbytes=sum(3 * B * v.ho * v.wo * v.cout * self.esz for v in grp))
+                        bset ^= 1
+                    if uid in batch_draw:
+                        draw, dkey = batch_draw[uid]
                     # one backward launch set for all members of the launch (segments:
                     # each member's upstream gradient slice, beta and dbeta)
                     pool_i = next((j for j, b in pool_bwd.items() if b == u.first.y.buf), None)
@@ -774,7 +855,7 @@ class Engine:
                                                             wsb, s),
                             "bn_relu_bwd", ln, [("d", pn.y.buf, pn.y.c_off), ("am", pool_i), ("r", uid), ("p",)],
                             d_all(pn.x) + [dkey, ("g", uid), ("ws", ln)], nbytes=4 * M * u.cout * self.esz)
-                    for grp in ([] if pool_i is not None else self._bn_groups(u)):
+                    for grp in ([] if pool_i is not None or uid in batch_draw else self._bn_groups(u)):
                         co0 = grp[0][1]
                         cg = sum(m.cout for m, _ in grp)
                         segs = (_ffi.BnSeg * len(grp))(*[
