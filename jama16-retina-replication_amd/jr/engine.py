@@ -1095,7 +1095,11 @@ class Engine:
         fwd, bwd, opt, _, _ = self._build_calls(B)
         torch.cuda.synchronize(self.device)
         _ffi.check("jr_graph_begin", self.lib.jr_graph_begin(self._s))
-        self._capturing = True
+        # the producer waits become the graph's edges (two lanes at most: with
+        # three, waits on events recorded mid-stream crashed hipGraphInstantiate
+        # on ROCm 7.2); JR_GRAPH_PRECISE=0: tail waits (bf16 replay 10.04 vs
+        # 9.28 ms per step, eager 9.31: profiles/r05_graph_probe.txt)
+        self._capturing = os.environ.get("JR_GRAPH_PRECISE", "1") == "0"
         try:
             self._fork()
             self._run(fwd)
