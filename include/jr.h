@@ -233,6 +233,19 @@ int jr_bn_stats(int dtype, const void* x, int64_t m, int32_t c, float eps, float
 int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,
                      const float* mean, const float* invstd, const float* beta, void* y, int32_t y_c_off,
                      int32_t y_c_stride, void* stream);
+/* BN + ReLU apply of a fused sibling launch's members in ONE launch: x
+ * spans the launch's c channels; segment i (channels [sum_{j<i} c_j, ... +
+ * c_i), sum c_i = c, each a multiple of 4 fp32 / 8 bf16) writes its own
+ * output slice with its own beta.  Per element bitwise jr_bn_relu_apply.
+ * 1 <= nseg <= 4. */
+typedef struct jr_bn_apply_seg {
+  void* y;
+  int32_t y_c_off, y_c_stride, c;
+  const float* beta;
+} jr_bn_apply_seg;
+int jr_bn_relu_apply_multi(int dtype, int nseg, const jr_bn_apply_seg* segs, const void* x, int32_t x_c_off,
+                           int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd,
+                           void* stream);
 /* jr_bn_relu_apply with the statistics finalize folded in: mean / invstd of
  * the c channels come from the single-stage partials of the producing conv
  * (jr_conv2d_fwd_bn_partials): part = ws + ws_offset, layout [2][n_total][P]

@@ -404,6 +404,59 @@ __global__ void __launch_bounds__(256) k_bn_relu_apply(const T* __restrict__ x, 
   }
 }
 
+// The apply of a fused sibling launch's members in ONE launch
+// (jr_bn_relu_apply_multi): the raw output's c channels, segment i its own
+// output slice and beta; per element exactly k_bn_relu_apply's arithmetic.
+struct ApplySegs {
+  void* y[kMaxSegs];
+  const float* beta[kMaxSegs];
+  int y_off[kMaxSegs], y_stride[kMaxSegs];
+  int c0[kMaxSegs + 1];
+  int n;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_bn_relu_apply_multi(const T* __restrict__ x, int xs, int64_t m, int c,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, ApplySegs sg) {
+  constexpr int VW = Vec<T>::N;
+  const int tpr = c / VW;
+  const int rpp = 256 / tpr;
+  const int t = threadIdx.x;
+  const int q = t % tpr, rr = t / tpr;
+  if (rr >= rpp) return;
+  int si = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxSegs; ++i) si += (i < sg.n && q * VW >= sg.c0[i]) ? 1 : 0;
+  const int lc = q * VW - sg.c0[si];
+  T* y = static_cast<T*>(sg.y[si]) + sg.y_off[si] + lc;
+  const int ys = sg.y_stride[si];
+  float mu[VW], is[VW], be[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    mu[j] = mean[q * VW + j]; is[j] = invstd[q * VW + j]; be[j] = sg.beta[si][lc + j];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpp * kAppUnroll + rr;
+  uint4 xr[kAppUnroll];
+#pragma unroll
+  for (int u = 0; u < kAppUnroll; ++u) {
+    const int64_t r = min(r0 + (int64_t)u * rpp, m - 1);
+    xr[u] = *reinterpret_cast<const uint4*>(x + r * xs + q * VW);
+  }
+#pragma unroll
+  for (int u = 0; u < kAppUnroll; ++u) pin(xr[u]);
+#pragma unroll
+  for (int u = 0; u < kAppUnroll; ++u) {
+    const int64_t r = r0 + (int64_t)u * rpp;
+    if (r >= m) break;
+    float xv[VW], o[VW];
+    Vec<T>::unpack(xr[u], xv);
+#pragma unroll
+    for (int j = 0; j < VW; ++j) o[j] = fmaxf(bn_pre(xv[j], mu[j], is[j], be[j]), 0.f);
+    Vec<T>::st(y + r * ys, o);
+  }
+}
+
 // k_bn_relu_apply with the statistics finalize folded in: block (bx, by)
 // first combines the conv's single-stage partials of the 32 channels of group
 // by (stats_combine8: 8 lanes per channel, bitwise what k_stats_finalize8
@@ -805,6 +858,44 @@ JR_API int jr_bn_relu_apply(int dtype, const void* x, int32_t x_c_off, int32_t x
   if (!check_slice(dtype, y_c_off, y_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_apply: bad output slice");
   return bn_apply_launch(dtype, 1, x, x_c_stride, 0, m, c, mean, invstd, 0, beta, 0, y, y_c_off, y_c_stride, 0,
                          as_stream(stream));
+}
+
+JR_API int jr_bn_relu_apply_multi(int dtype, int nseg, const jr_bn_apply_seg* segs, const void* x, int32_t x_c_off,
+                                  int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd,
+                                  void* stream) {
+  int rc = check_common(dtype, m, c);
+  if (rc) return rc;
+  if (!segs || nseg < 1 || nseg > kMaxSegs) return fail(JR_ERR_INVALID, "bn_relu_apply_multi: 1..4 segments");
+  if (!x || !mean || !invstd) return fail(JR_ERR_INVALID, "bn_relu_apply_multi: null pointer");
+  if (!check_slice(dtype, x_c_off, x_c_stride, c)) return fail(JR_ERR_INVALID, "bn_relu_apply_multi: bad input slice");
+  ApplySegs sg{};
+  sg.n = nseg;
+  int c0 = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const jr_bn_apply_seg& e = segs[i];
+    if (!e.y || !e.beta) return fail(JR_ERR_INVALID, "bn_relu_apply_multi: null pointer in a segment");
+    if (e.c <= 0 || e.c % vec_width(dtype) || !check_slice(dtype, e.y_c_off, e.y_c_stride, e.c))
+      return fail(JR_ERR_INVALID, "bn_relu_apply_multi: bad output segment");
+    sg.y[i] = e.y;
+    sg.beta[i] = e.beta;
+    sg.y_off[i] = e.y_c_off;
+    sg.y_stride[i] = e.y_c_stride;
+    sg.c0[i] = c0;
+    c0 += e.c;
+  }
+  if (c0 != c) return fail(JR_ERR_INVALID, "bn_relu_apply_multi: segment channels must sum to c");
+  sg.c0[nseg] = c;
+  const size_t esz = dtype == JR_BF16 ? 2 : 4;
+  x = static_cast<const char*>(x) + (size_t)x_c_off * esz;
+  const dim3 grid(apply_grid(m, c, vec_width(dtype)));
+  hipStream_t s = as_stream(stream);
+  if (dtype == JR_F32)
+    hipLaunchKernelGGL(k_bn_relu_apply_multi<float>, grid, dim3(256), 0, s, (const float*)x, x_c_stride, m, c, mean,
+                       invstd, sg);
+  else
+    hipLaunchKernelGGL(k_bn_relu_apply_multi<uint16_t>, grid, dim3(256), 0, s, (const uint16_t*)x, x_c_stride, m, c,
+                       mean, invstd, sg);
+  return check_launch("bn_relu_apply_multi");
 }
 
 JR_API int jr_bn_relu_apply_stats(int dtype, const void* x, int32_t x_c_off, int32_t x_c_stride, int64_t m, int32_t c,

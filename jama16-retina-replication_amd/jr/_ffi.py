@@ -52,6 +52,11 @@ class BnSeg(Structure):
                 ("beta", c_void_p), ("dbeta", c_void_p)]
 
 
+class BnApplySeg(Structure):
+    """include/jr.h jr_bn_apply_seg: one member's output slice and beta."""
+    _fields_ = [("y", c_void_p), ("y_c_off", c_int32), ("y_c_stride", c_int32), ("c", c_int32), ("beta", c_void_p)]
+
+
 class BnBwdLayer(Structure):
     """include/jr.h jr_bn_bwd_layer: one layer of a batched BN backward."""
     _fields_ = [("nseg", c_int32), ("segs", BnSeg * 4), ("x", c_void_p), ("x_c_off", c_int32),
@@ -130,6 +135,8 @@ _SIGS = {
     "jr_comm_destroy": (c_int, [c_void_p]),
     "jr_bn_workspace_size": (c_size_t, [c_int64, c_int32]),
     "jr_bn_relu_bwd_batch_workspace_size": (c_size_t, [c_int32, c_void_p]),
+    "jr_bn_relu_apply_multi": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int32,
+                                       c_void_p, c_void_p, c_void_p]),
     "jr_bn_relu_bwd_batch": (c_int, [c_int, c_int32, c_void_p, c_void_p, c_size_t, c_void_p]),
     "jr_bn_stats": (c_int, [c_int, c_void_p, c_int64, c_int32, c_float, c_void_p, c_void_p,
                             c_void_p, c_size_t, c_void_p]),

@@ -154,6 +154,10 @@ class Engine:
         # path to the next layer's BN backward) before the filter gradient
         # (JR_DGRAD_FIRST=0: filter gradient first)
         self.dgrad_first = os.environ.get("JR_DGRAD_FIRST", "1") != "0"
+        # a fused sibling launch's members' BN + ReLU in one launch
+        # (JR_APPLY_MULTI=0: one launch per member, for A/B runs)
+        self.apply_multi = os.environ.get("JR_APPLY_MULTI", "1") != "0"
+        self._vw = 8 if dtype == "bf16" else 4          # channels per 16-byte vector (one launch: <= 256 per row)
         self.plan = build_plan(self.g, fuse_siblings)
         # conv2d_bn outputs read only by a max-pool (the stem's conv2d_3 and
         # conv2d_5): BN + ReLU run inside the pool (jr_bn_relu_maxpool3x3s2_fwd)
@@ -680,6 +684,19 @@ class Engine:
                                                     self.mean_unit[uid].data_ptr(),
                                                     self.invstd_unit[uid].data_ptr(), ws, wsb, s),
                     "conv_fwd", ln, ax_reads(u.x) + [wkey], [("r", uid), ("ws", ln)])
+                if (self.apply_multi and len(u.members) > 1 and u.cout // self._vw <= 256
+                        and not any(m.y.buf in fused_bufs for m in u.members)):
+                    # every member's BN + ReLU in one launch (jr_bn_relu_apply_multi)
+                    segs = (_ffi.BnApplySeg * len(u.members))(*[
+                        _ffi.BnApplySeg(A(m.y.buf), m.y.c_off, g.bufs[m.y.buf].c, m.cout,
+                                        self._p(f"batch_normalization_{m.idx + 1}/beta")) for m in u.members])
+                    keep.append(segs)
+                    add(fwd, L.jr_bn_relu_apply_multi, (dt, len(u.members), ctypes.byref(segs), raw, 0, u.cout, M,
+                                                        u.cout, self.mean_unit[uid].data_ptr(),
+                                                        self.invstd_unit[uid].data_ptr(), s),
+                        "bn_relu", ln, [("r", uid), ("p",)], [("a", m.y.buf, m.y.c_off) for m in u.members],
+                        nbytes=2 * M * u.cout * self.esz)
+                    continue
                 for m, co in zip(u.members, u.col_off):
                     if m.y.buf in fused_bufs:
                         continue        # applied inside its max-pool
