@@ -127,9 +127,13 @@ class Engine:
         self.adam_b1p, self.adam_b2p = np.float32(self.adam_b1), np.float32(self.adam_b2)
         self.head_mode = _ffi.JR_HEAD_SIGMOID if head == "sigmoid" else _ffi.JR_HEAD_SOFTMAX
         self.units = self.g.units
-        # (diagnostic) JR_LANE_PRIORITY="p0,p1,...": HIP stream priority per lane
-        # (lower = higher priority); default: all normal
-        prio = [int(v) for v in os.environ.get("JR_LANE_PRIORITY", "").split(",") if v.strip()]
+        # JR_LANE_PRIORITY="p0,p1,...": HIP stream priority per lane (lower =
+        # higher priority). Default: lane 0 (the trunk) high for fp32 steps,
+        # measured 0.1 ms/step faster over 6 interleaved rounds on two boxes
+        # (profiles/r05_ab_prio_f32*.txt); all normal for bf16, where it
+        # measured neutral. Priority moves no result: scheduling only.
+        prio_def = "-1,0" if self.dt == _ffi.JR_F32 else ""
+        prio = [int(v) for v in os.environ.get("JR_LANE_PRIORITY", prio_def).split(",") if v.strip()]
         prio += [0] * max(0, int(lanes) - len(prio))
         self.stream = torch.cuda.Stream(device=self.device, priority=prio[0])
         self._s = ctypes.c_void_p(self.stream.cuda_stream)
