@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-defer-wgrad", action="store_true",
-                    help="reduce each split-K filter gradient right after its GEMM (A/B of jr_wgrad_reduce)")
+                    help="reduce each split-K filter gradient right after its GEMM (already the fp32 default; bf16 defers to one jr_wgrad_reduce)")
     return ap.parse_args()
 
 
@@ -447,7 +447,7 @@ def main():
     B, res = args.batch or (64 if train else 32), args.res
     math = args.conv_math if args.dtype == "f32" else "bf16"
     eng = Engine(B, res, res, device=local, dtype=args.dtype, seed=0, lanes=args.lanes, train=train,
-                 conv_math=math, tiles=args.tiles, defer_wgrad=not args.no_defer_wgrad)
+                 conv_math=math, tiles=args.tiles, defer_wgrad=False if args.no_defer_wgrad else None)
     imgs = synth.fundus_batch(rank * B, B, res)
     labels = synth.labels(rank * B, B)
     eng.set_batch(imgs, labels)

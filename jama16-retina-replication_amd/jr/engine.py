@@ -89,7 +89,7 @@ class Engine:
                  optimizer: str = "nesterov", lr: float = 3e-3, momentum: float = 0.9,
                  head: str = "sigmoid", seed: int = 0, graph: Optional[Graph] = None,
                  autotune: bool = False, tiles: str = "pinned", fuse_siblings: bool = True, lanes: int = 2,
-                 conv_math: Optional[str] = None, defer_wgrad: bool = True, fuse_pool: Optional[bool] = None,
+                 conv_math: Optional[str] = None, defer_wgrad: Optional[bool] = None, fuse_pool: Optional[bool] = None,
                  fold_stats: Optional[bool] = None):
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
@@ -188,6 +188,14 @@ class Engine:
         # filter gradients of split-K wgrad GEMMs: slabs kept per layer and
         # summed by ONE jr_wgrad_reduce launch per flush point (the end of the
         # backward, and each gradient bucket's issue point: set_flush_points)
+        # Default (None): deferred for bf16; fp32 reduces each layer's slabs
+        # right after its filter-gradient GEMM (bitwise the same sums), which
+        # with producer waits overlaps the other lane: 24.30 -> 24.06 ms per
+        # step, bf16 9.25 -> 9.30 the other way (profiles/r05_ab_defer*.txt).
+        # JR_DEFER_WGRAD=0/1 overrides the default.
+        if defer_wgrad is None:
+            env = os.environ.get("JR_DEFER_WGRAD", "")
+            defer_wgrad = env == "1" if env in ("0", "1") else self.dt != _ffi.JR_F32
         self.defer_wgrad = bool(defer_wgrad)
         self._flush_points: List[int] = []
         self._graphs: Dict[int, int] = {}

@@ -244,9 +244,9 @@ def test_deferred_wgrad_reduce_is_bitwise(dtype):
     imgs = synth.fundus_batch(4, 4, 139)
     y = np.array([[1.0], [0.0], [0.0], [1.0]], np.float32)
     ref = Engine(4, 139, 139, seed=8, dtype=dtype, defer_wgrad=False)
-    dfr = Engine(4, 139, 139, seed=8, dtype=dtype)
-    pts = Engine(4, 139, 139, seed=8, dtype=dtype)
-    gr = Engine(4, 139, 139, seed=8, dtype=dtype)
+    dfr = Engine(4, 139, 139, seed=8, dtype=dtype, defer_wgrad=True)
+    pts = Engine(4, 139, 139, seed=8, dtype=dtype, defer_wgrad=True)
+    gr = Engine(4, 139, 139, seed=8, dtype=dtype, defer_wgrad=True)
     pts.set_flush_points([pts.nparam // 2, pts.nparam // 5, pts.nparam // 20])
     _, bwd, _, _, _ = pts._build_calls(4)
     assert sum(c.name == "wgrad_reduce" for c in bwd) >= 2
