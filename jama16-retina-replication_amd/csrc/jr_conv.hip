@@ -799,16 +799,20 @@ static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
 constexpr int kSkBlocks = 512;     // stream-K grid: 2 x 256 CUs
 constexpr int kSkMinIters = 4;     // K-tiles per stream-K block at least
 
-// Blocks the planner's split-K factor aims for (>= 2.5 per CU); filter
-// gradients may aim lower (JR_WGRAD_SPLIT_TARGET, an A/B knob read once):
-// their slabs are summed by the deferred k_wgrad_reduce from HBM.
-static int split_target(int op) {
+// Blocks the planner's split-K factor aims for (>= 2.5 per CU). x8 filter
+// gradients aim for 384: their slabs are summed per layer on the GEMM's lane
+// (the fp32 engine default), and fewer slabs measured 0.12-0.14 ms per step
+// faster on two boxes (profiles/r05_ab_wsplit*_f32.txt; 320 / 1,024 slower,
+// bf16 at 384 slower). JR_WGRAD_SPLIT_TARGET overrides it (A/B knob, read once).
+static int split_target(int dtype, int op) {
   static const int wg = [] {
     const char* e = std::getenv("JR_WGRAD_SPLIT_TARGET");
     const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : 640;
+    return v > 0 ? v : 0;
   }();
-  return op == OP_WGRAD ? wg : 640;
+  if (op != OP_WGRAD) return 640;
+  if (wg > 0) return wg;
+  return dtype == JR_F32_X8 || dtype == JR_F32_X8P ? 384 : 640;
 }
 
 static Plan plan_with(int dtype, int cfg, int M, int N, int K, int op) {
@@ -820,7 +824,7 @@ static Plan plan_with(int dtype, int cfg, int M, int N, int K, int op) {
   p.ktiles = (int)ceil_div(K, t.bk);
   const int tiles = p.mt * p.nt;
   int splits = 1;
-  const int target = split_target(op);
+  const int target = split_target(dtype, op);
   if (tiles < target) {
     splits = (int)ceil_div(target, tiles);
     const int max_by_k = std::max(1, p.ktiles / 8);
