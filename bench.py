@@ -77,6 +77,11 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=64)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--dp", default="auto", choices=["auto", "on", "off"],
+                    help="bucketed gradient all-reduce in the step (jr.dist.BucketAllReduce): auto = only when "
+                         "WORLD_SIZE > 1; on = also at N=1, over a world-1 RCCL group (the DP step timed on one GPU)")
+    ap.add_argument("--dp-transport", default="torch", choices=["torch", "jr"],
+                    help="torch.distributed all_reduce (backend nccl = RCCL) or libjr's own RCCL communicator")
     ap.add_argument("--no-defer-wgrad", action="store_true",
                     help="reduce each split-K filter gradient right after its GEMM (already the fp32 default; bf16 defers to one jr_wgrad_reduce)")
     return ap.parse_args()
@@ -262,14 +267,32 @@ def dist_setup(args):
     backend = os.environ.get("JR_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or getattr(args, "dp", "auto") == "on":
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:      # world-1 group, no launcher
+            import socket
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            sk.close()
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
     return rank, world, local, dist
+
+
+def gather_devices(dist, local: int) -> list:
+    """The device index of every rank (n_gpus counts distinct devices: a
+    rehearsal with every rank on cuda:0 is one GPU)."""
+    if not dist or dist.get_world_size() == 1:
+        return [local]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, local)
+    return out
 
 
 def max_over_ranks(dist, v: float) -> float:
@@ -398,6 +421,8 @@ def ensemble_bench(args) -> dict:
                               f"({nconv} launches/forward)",
                     "conv_ms_per_forward": round(tconv * 1e3, 3),
                     "algorithmic_gflop_per_forward": round(flops / 1e9, 1)}
+        devices = len({int(v) for v in gather_devices(dist, local)})
+        rehearsal = world > 1 and (devices < world or dist.get_backend() != "nccl")
         if dist:
             dist.barrier()
     finally:
@@ -406,7 +431,8 @@ def ensemble_bench(args) -> dict:
     M = args.members
     out = {
         "metric": f"ensemble eval images/sec, Inception-v3 {res}^2, {M} members, batch {B} (evaluate.py -lm)",
-        "value": round(n / t_all, 2), "unit": "images/sec", "n_gpus": world, "steps": 1, "warmup": 1,
+        "value": round(n / t_all, 2), "unit": "images/sec", "n_gpus": devices, "rehearsal": rehearsal,
+        "steps": 1, "warmup": 1,
         "ms_per_step": round(t_all / -(-n // (B * world)) * 1e3, 3), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": args.dtype,
         "data": f"{n} synthetic fundus-shaped JPEG q=100 TFRecords at {res}x{res} (jr.synth_records), random Keras "
@@ -430,12 +456,27 @@ def ensemble_bench(args) -> dict:
     return out if rank == 0 else None
 
 
+def _stdout_for_json_only() -> int:
+    """Keep stdout for the ONE JSON line: everything else written to fd 1
+    (RCCL prints its version banner to C stdout when a communicator comes
+    up) goes to stderr; returns the fd the JSON line is written to."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return fd
+
+
+def emit(fd: int, out: dict) -> None:
+    os.write(fd, (json.dumps(out) + "\n").encode())
+
+
 def main():
     args = parse()
+    json_fd = _stdout_for_json_only()
     if args.mode == "ensemble":
         out = ensemble_bench(args)
         if out is not None:
-            print(json.dumps(out), flush=True)
+            emit(json_fd, out)
         return
     rank, world, local, dist = dist_setup(args)
 
@@ -453,7 +494,13 @@ def main():
     eng.set_batch(imgs, labels)
     eng.synchronize()
     log(f"engine ready (rank {rank}/{world})")
-    ar = BucketAllReduce(eng, world) if world > 1 and train else None
+    ar = None
+    if train and (world > 1 or args.dp == "on") and args.dp != "off":
+        comm = None
+        if args.dp_transport == "jr":
+            from jr.dist import JrComm
+            comm = JrComm.from_torch_group(rank, world, local)
+        ar = BucketAllReduce(eng, world, comm=comm)
     use_graph = False
 
     def step():
@@ -480,6 +527,8 @@ def main():
     if not np.isfinite(loss):
         raise SystemExit(f"non-finite {'loss' if train else 'prediction'} {loss}")
 
+    devices = len({int(v) for v in gather_devices(dist, local)})
+    rehearsal = world > 1 and (devices < world or dist.get_backend() != "nccl")
     out = None
     if rank == 0:
         imgs_s = B * world * args.steps / elapsed
@@ -501,7 +550,7 @@ def main():
         out = {
             "metric": (f"train images/sec, Inception-v3 {res}^2 bs{B}/GPU" if train else
                        f"eval images/sec, Inception-v3 {res}^2 bs{B}/GPU (one ensemble member, batch-stat BN)"),
-            "value": round(imgs_s, 2), "unit": "images/sec", "n_gpus": world,
+            "value": round(imgs_s, 2), "unit": "images/sec", "n_gpus": devices,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.dtype, "data": f"synthetic fundus-shaped uint8 {res}x{res}x3 (jr.synth), random Keras init",
@@ -509,17 +558,24 @@ def main():
                                     f"Nesterov lr 3e-3 m 0.9" if train else
                                     f"Inception-v3 {res}x{res} {args.dtype} forward (evaluate.py), batch {B}/GPU, "
                                     f"batches sharded over ranks"), "model": "inception_v3", "global_batch": B * world,
-                       "seq_len": None, "parallelism": f"dp{world}", "hip_graph": use_graph, "lanes": args.lanes,
+                       "seq_len": None, "parallelism": f"dp{world}", "ranks": world, "hip_graph": use_graph,
+                       "lanes": args.lanes,
+                       "allreduce": (None if ar is None else
+                                     {"transport": "jr_comm (RCCL)" if ar.comm is not None else
+                                      f"torch.distributed {dist.get_backend()}", "buckets": len(ar.buckets),
+                                      "payload": ar.payload, "fenced_issue_points_per_step": ar.fences,
+                                      "world": world}),
                        "tiles": eng.tiles,
                        "conv_math": CONV_MATH[args.conv_math] if args.dtype == "f32" else "bf16 MFMA"},
             ("final_loss" if train else "mean_prediction"): round(loss, 5),
+            "rehearsal": rehearsal,
             "roofline": roof,
             "hbm_families": hbm,
         }
         if not args.no_cpu_baseline and world == 1 and train:
             log("cpu baseline")
             out["cpu_baseline"] = cpu_baseline(args, res)
-        print(json.dumps(out), flush=True)
+        emit(json_fd, out)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

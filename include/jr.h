@@ -96,14 +96,17 @@ const char* jr_last_error(void);
 const char* jr_version(void);
 /* Device-side failures of the launches on the CURRENT device since the last
  * check (call it after synchronising the streams that ran them): JR_OK, or
- * JR_ERR_DEVICE when a kernel counted a failure into the library's device
- * error word -- today a stream-K hand-off count found past its tile's piece
- * count (a hand-off word that was not left zero; the tile's output is then
- * invalid).  Stream-K blocks never wait for one another, so no timeout
- * exists.  On JR_ERR_DEVICE the call synchronises the device, re-zeroes every
- * stream-K hand-off word and the error word, so the NEXT launches are
- * correct.  Host-synchronising (one 4-byte copy; the repair path a device
- * sync). */
+ * JR_ERR_DEVICE when a stream-K hand-off word was not left zero: either a
+ * kernel counted a count found past its tile's piece count into the
+ * library's device error word, or a hand-off word of a stream with no work
+ * in flight is non-zero (a stale count below the piece count, which makes a
+ * tile complete early; the words of every idle stream are scanned here).
+ * The outputs of the launches since the last check are then invalid.
+ * Stream-K blocks never wait for one another, so no timeout exists.  On
+ * JR_ERR_DEVICE the call synchronises the device, re-zeroes every stream-K
+ * hand-off word and the error word, so the NEXT launches are correct.
+ * Host-synchronising (a 4-byte copy plus the used hand-off words of each
+ * idle stream; the repair path a device sync). */
 int jr_device_check(void);
 /* Diagnostics (tests): set every stream-K hand-off word of `stream` (the
  * current device's) to `value`, in stream order -- the next stream-K launch

@@ -18,6 +18,7 @@ namespace {
 struct Scratch {
   unsigned* p = nullptr;
   size_t words = 0;
+  size_t used = 0;      // the most words any launch on the stream has asked for
 };
 std::mutex g_scratch_mu;
 std::map<std::tuple<int, hipStream_t, int>, Scratch> g_scratch;
@@ -80,6 +81,7 @@ unsigned* stream_scratch(hipStream_t s, int kind, size_t words) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   Scratch& e = g_scratch[std::make_tuple(dev, s, kind)];
+  e.used = std::max(e.used, words);
   if (e.words < words) {
     const size_t n = std::max<size_t>(words, std::max<size_t>(2 * e.words, 16384));
     unsigned* p = scratch_alloc(s, n);
@@ -91,14 +93,16 @@ unsigned* stream_scratch(hipStream_t s, int kind, size_t words) {
   return e.p;
 }
 
-unsigned* device_error_word() {
+unsigned* device_error_word(hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
   {
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     if (g_err_word[dev]) return g_err_word[dev];
   }
-  if (capturing(nullptr, nullptr)) return nullptr;   // (jr_init allocates it before any capture)
+  // the launch's own stream capturing: no synchronous allocation now (it would
+  // break a global-mode capture); the caller reports "call jr_init first"
+  if (capturing(s, nullptr)) return nullptr;
   return err_word_init(dev) == JR_OK ? g_err_word[dev] : nullptr;
 }
 
@@ -142,7 +146,30 @@ JR_API int jr_device_check(void) {
   unsigned h = 0;
   hipError_t e = hipMemcpy(&h, w, sizeof(unsigned), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("jr_device_check: ") + hipGetErrorString(e));
-  if (h == 0) return JR_OK;
+  // every hand-off word of an idle stream must be back at zero: a launch
+  // whose counts completed leaves its words zero, so a word found non-zero
+  // there is a stale count -- below its piece count it made a tile complete
+  // early (summing unpublished slots) without tripping the in-kernel check
+  // (ADVICE r05); streams with work in flight are checked at a later call
+  size_t stale = 0;
+  {
+    std::vector<std::pair<hipStream_t, Scratch>> idle;
+    {
+      std::lock_guard<std::mutex> lk(g_scratch_mu);
+      for (auto& kv : g_scratch)
+        if (std::get<0>(kv.first) == dev && std::get<2>(kv.first) == 0 && kv.second.p && kv.second.used)
+          idle.emplace_back(std::get<1>(kv.first), kv.second);
+    }
+    std::vector<unsigned> buf;
+    for (auto& [st, sc] : idle) {
+      if (hipStreamQuery(st) != hipSuccess) continue;       // busy (or not a live stream): not now
+      buf.resize(sc.used);
+      e = hipMemcpy(buf.data(), sc.p, sc.used * sizeof(unsigned), hipMemcpyDeviceToHost);
+      if (e != hipSuccess) return fail(JR_ERR_HIP, std::string("jr_device_check: ") + hipGetErrorString(e));
+      for (unsigned v : buf) stale += v != 0;
+    }
+  }
+  if (h == 0 && stale == 0) return JR_OK;
   // repair: every launch has finished, then the hand-off words of every
   // stream of this device and the error word go back to 0
   e = hipDeviceSynchronize();
@@ -156,9 +183,9 @@ JR_API int jr_device_check(void) {
   (void)hipMemset(w, 0, sizeof(unsigned));
   (void)hipDeviceSynchronize();
   return fail(JR_ERR_DEVICE, "stream-K hand-off: " + std::to_string(h) +
-                                 " count(s) found past their tile's piece count (a hand-off word not left zero); the "
-                                 "outputs of the launches since the last jr_device_check are invalid (hand-off words "
-                                 "reset)");
+                                 " count(s) found past their tile's piece count and " + std::to_string(stale) +
+                                 " hand-off word(s) of idle streams not left zero; the outputs of the launches since "
+                                 "the last jr_device_check are invalid (hand-off words reset)");
 }
 
 JR_API int jr_debug_poison_sk_counts(void* stream, uint32_t value) {

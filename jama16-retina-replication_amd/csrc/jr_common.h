@@ -26,7 +26,7 @@ unsigned* stream_scratch(hipStream_t s, int kind, size_t words);
 // The current device's error word (jr_api.cpp): kernels count device-side
 // failures into it (vector atomics); jr_device_check() reads, reports and
 // clears it.  Allocated by jr_init (or on first use outside a capture).
-unsigned* device_error_word();
+unsigned* device_error_word(hipStream_t s);
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

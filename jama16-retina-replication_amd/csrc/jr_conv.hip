@@ -1149,7 +1149,7 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     if (!a.sk_flags) return fail(JR_ERR_HIP, "conv: stream-K flag words could not be allocated");
     a.sk_fmb = (long long)p.sk_blocks * sizeof(unsigned);
     // a hand-off count found past its piece count (a word not left zero) is reported here
-    a.sk_err = device_error_word();
+    a.sk_err = device_error_word(s);
     if (!a.sk_err) return fail(JR_ERR_HIP, "conv: no device error word (call jr_init before capturing)");
     grid = dim3(p.sk_blocks, members, 1);
   }

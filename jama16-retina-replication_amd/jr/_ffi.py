@@ -270,9 +270,10 @@ def check(name: str, rc: int) -> None:
 
 def device_check() -> None:
     """jr_device_check on the current device (after the caller synchronised
-    its streams): raise JRError when a launch reported a device-side failure
-    (a stream-K hand-off that timed out); the library has then reset its
-    hand-off flags, so later launches are correct again."""
+    its streams): raise JRError when a stream-K hand-off count word was not
+    left zero (counted past its piece count by a launch, or found stale on an
+    idle stream); the library has then reset its hand-off words, so later
+    launches are correct again."""
     check("jr_device_check", load().jr_device_check())
 
 

@@ -12,9 +12,12 @@ boundaries, issued in reverse layer order: backward produces gradients from
 the last layer to the first, so when conv k's filter gradient is done every
 byte at offsets >= offset(conv k) is final and any bucket lying entirely in
 that range is launched immediately (async), overlapping the remaining
-backward kernels.  RCCL runs on its own stream and is ordered after the
-engine stream's work at issue time; `finish` makes the engine stream wait
-for every bucket before the optimizer.  The mean (1/world) is folded into
+backward kernels.  At an issue point with work, a stream outside the
+engine's lanes (the feed stream of the torch transport, the comm stream of
+JrComm) waits for every lane's work so far (Engine.fence_lanes) and the
+all-reduce is issued from it; the lanes themselves never wait for each other
+or for the exchange until `finish` makes lane 0 wait for every bucket before
+the optimizer (an issue point without a ready bucket costs nothing).  The mean (1/world) is folded into
 the optimizer launch as grad_scale.  Weights stay bitwise identical across
 ranks because every rank applies the same update to the same reduced
 gradient.
@@ -22,9 +25,9 @@ gradient.
 Two transports, same bucket walk:
   * torch.distributed all_reduce (backend 'nccl' = RCCL; 'gloo' on CPU);
   * libjr's own RCCL communicator (JrComm: jr_comm_init / jr_allreduce_sum,
-    include/jr.h) on a dedicated comm stream that waits for the engine
-    stream at each bucket's issue point; the engine stream waits for the
-    comm stream before the optimizer.
+    include/jr.h) on a dedicated comm stream that waits for every lane at
+    each bucket's issue point; lane 0 waits for the comm stream before the
+    optimizer.
 and two payloads: fp32 (default; the sum of fp32 gradients) or bf16 (43.5 MB
 instead of 87.1 MB: each bucket cast to bf16, summed in bf16 by RCCL, cast
 back; ranks stay identical, the sum carries bf16 rounding).
@@ -163,16 +166,38 @@ class BucketAllReduce:
                      if payload == "bf16" else None)
         if comm is not None:
             self.comm_stream = torch.cuda.Stream(device=engine.grads.device)
-            self._ready_ev = torch.cuda.Event()
             self._done_ev = torch.cuda.Event()
+        # torch transport: buckets are issued from a feed stream that waits
+        # for every lane at the issue point (Engine.fence_lanes); the lanes
+        # never wait for each other or for the all-reduce until finish()
+        self.feed = (torch.cuda.Stream(device=engine.grads.device)
+                     if comm is None and getattr(engine, "stream", None) is not None else None)
+        self.fences = 0                 # issue points that fenced the lanes (one per issue point with work)
 
     def begin(self, eng=None) -> None:
         self.works = []
         self.next = 0
+        self.fences = 0
 
     def _stream_ctx(self):
         s = getattr(self.eng, "stream", None)
         return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
+
+    def _feed_ctx(self):
+        return torch.cuda.stream(self.feed) if self.feed is not None else contextlib.nullcontext()
+
+    def _fence(self, stream) -> None:
+        """`stream` waits for every gradient enqueued so far on any lane
+        (no stream: a host-side replica, nothing to order)."""
+        eng = self.eng
+        if stream is not None:
+            if hasattr(eng, "fence_lanes"):
+                eng.fence_lanes(stream)
+            else:
+                ev = torch.cuda.Event()
+                ev.record(eng.stream)
+                stream.wait_event(ev)
+        self.fences += 1
 
     def _cast(self, fn, src: int, dst: int, n: int, stream) -> None:
         _ffi.check(fn, getattr(_ffi.load(), fn)(ctypes.c_void_p(src), ctypes.c_void_p(dst), n,
@@ -180,8 +205,6 @@ class BucketAllReduce:
 
     def _issue_jr(self, lo: int, hi: int) -> None:
         eng, cs = self.eng, self.comm_stream
-        self._ready_ev.record(eng.stream)           # the bucket's gradients are final on the engine stream
-        cs.wait_event(self._ready_ev)
         g = eng.grads.data_ptr() + 4 * lo
         if self.half is None:
             self.comm.allreduce(g, hi - lo, _ffi.JR_F32, cs.cuda_stream)
@@ -193,17 +216,24 @@ class BucketAllReduce:
 
     def _issue_torch(self, lo: int, hi: int):
         eng = self.eng
-        with self._stream_ctx():
+        with self._feed_ctx():
             if self.half is None:
                 return dist.all_reduce(eng.grads[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            st = eng.stream.cuda_stream if getattr(eng, "stream", None) is not None else 0
+            st = self.feed.cuda_stream if self.feed is not None else 0
             self._cast("jr_cast_f32_to_bf16", eng.grads.data_ptr() + 4 * lo, self.half.data_ptr() + 2 * lo,
                        hi - lo, st)
             w = dist.all_reduce(self.half[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             return (w, lo, hi)
 
+    def ready(self, ready_from: int) -> bool:
+        """Whether param_ready(ready_from) issues at least one bucket."""
+        return self.next < len(self.buckets) and self.buckets[self.next][0] >= ready_from
+
     def _issue_ready(self, ready_from: int) -> None:
-        while self.next < len(self.buckets) and self.buckets[self.next][0] >= ready_from:
+        if not self.ready(ready_from):
+            return                      # nothing to issue: no fence, no wait anywhere
+        self._fence(self.comm_stream if self.comm is not None else self.feed)
+        while self.ready(ready_from):
             lo, hi = self.buckets[self.next]
             if self.comm is not None:
                 self._issue_jr(lo, hi)

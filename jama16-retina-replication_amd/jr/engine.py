@@ -975,8 +975,10 @@ class Engine:
     def _run(self, calls, events=None, hook: Optional[Callable[[int], None]] = None) -> None:
         for c in calls:
             if c.fn == "param_ready":
+                # no join here: the hook fences the lanes onto ITS stream, and
+                # only when a bucket is actually issued (fence_lanes); lane 0
+                # never waits for lane 1 at a conv unit
                 if hook is not None:
-                    self._join()            # the bucket's gradients may come from any lane
                     hook(c.args)
                 continue
             st = self.lane_streams[c.lane]
@@ -1028,6 +1030,17 @@ class Engine:
         for ev, st in zip(self._join_ev, self.lane_streams[1:]):
             ev.record(st)
             self.stream.wait_event(ev)
+
+    def fence_lanes(self, stream) -> None:
+        """`stream` (a consumer outside the lanes: the gradient all-reduce's
+        stream) waits for the work enqueued on EVERY lane so far; the lanes
+        themselves wait for nothing.  Used by jr.dist.BucketAllReduce at each
+        bucket's issue point instead of joining the lanes onto lane 0."""
+        if not hasattr(self, "_fence_ev"):
+            self._fence_ev = [torch.cuda.Event() for _ in range(self.nlanes)]
+        for ev, st in zip(self._fence_ev, self.lane_streams):
+            ev.record(st)
+            stream.wait_event(ev)
 
     # ------------------------------------------------------------------- data
     def set_batch(self, images, labels=None, n: Optional[int] = None) -> int:
@@ -1148,8 +1161,8 @@ class Engine:
 
     def synchronize(self) -> None:
         """Wait for every lane, then jr_device_check: a device-side failure
-        of any launch since the last check (a stream-K hand-off that timed
-        out) raises JRError here instead of leaving wrong numbers."""
+        of any launch since the last check (a stream-K hand-off count word not
+        left zero) raises JRError here instead of leaving wrong numbers."""
         for st in self.lane_streams:
             st.synchronize()
         _ffi.device_check()

@@ -43,9 +43,17 @@ class _RoundBF16(torch.autograd.Function):
 class InceptionV3Ref:
     """Functional Inception-v3 over a {name: tensor} parameter dict (HWIO)."""
 
-    def __init__(self, params: dict, dtype=torch.float64, requires_grad=True, emulate_bf16=False):
+    def __init__(self, params: dict, dtype=torch.float64, requires_grad=True, emulate_bf16=False,
+                 order_seed=None):
         self.dtype = dtype
         self.bf16 = emulate_bf16
+        # order_seed: the same arithmetic with every reduction in another fp32
+        # order -- each conv's input channels permuted (its Cin sum and the
+        # data-gradient's channel order), the images of each batch permuted
+        # (BN statistics, filter gradients, the loss mean).  Exact in real
+        # arithmetic; an independent fp32 sample of the loss curve for the
+        # calibration of the fp32 curve bar (oracle/make_golden.py curvecal)
+        self.order = np.random.default_rng(order_seed) if order_seed is not None else None
         self.P = {k: torch.tensor(np.asarray(v), dtype=dtype, requires_grad=requires_grad)
                   for k, v in params.items()}
         self._k = 0
@@ -58,6 +66,9 @@ class InceptionV3Ref:
         beta = self.P[f"batch_normalization_{self._k}/beta"]
         assert tuple(w.shape) == (num_row, num_col, x.shape[1], filters), (self._k, tuple(w.shape))
         pad = ((num_row - 1) // 2, (num_col - 1) // 2) if padding == "same" else (0, 0)
+        if self.order is not None:
+            perm = torch.as_tensor(self.order.permutation(x.shape[1]))
+            x, w = x[:, perm], w[:, :, perm, :]
         y = F.conv2d(x, self._r(w).permute(3, 2, 0, 1), stride=strides, padding=pad)
         y = self._r(y)                                                  # raw output as stored
         mean = y.mean(dim=(0, 2, 3), keepdim=True)
@@ -141,6 +152,10 @@ class InceptionV3Ref:
         Returns (loss, probs, grads{name: ndarray})."""
         for p in self.P.values():
             p.grad = None
+        if self.order is not None:
+            bp = self.order.permutation(len(x_nhwc))
+            x_nhwc = np.asarray(x_nhwc)[bp]
+            labels = np.asarray(labels).reshape(len(bp), -1)[bp]
         logits, probs, loss = self.forward(x_nhwc, labels)
         self.last_logits = logits.detach().cpu().numpy().copy()
         loss.backward()

@@ -109,15 +109,17 @@ def grad_projection(g, i):
     return float(np.dot(np.asarray(g, np.float64).ravel(), r))
 
 
-def _net(res, batch, seed, steps=1, cycle=None, dtype="float64", proj=False, bf16=False):
+def _net(res, batch, seed, steps=1, cycle=None, dtype="float64", proj=False, bf16=False, order_seed=None,
+         threads=None):
     import torch
     from jr import synth
     from jr.inception import build_inception_v3
     from jr.init import init_params, unflatten
     from oracle.inception_ref import InceptionV3Ref
-    torch.set_num_threads(os.cpu_count() or 8)
+    torch.set_num_threads(threads or os.cpu_count() or 8)
     g = build_inception_v3(res, res)
-    ref = InceptionV3Ref(unflatten(g, init_params(g, seed)), getattr(torch, dtype), emulate_bf16=bf16)
+    ref = InceptionV3Ref(unflatten(g, init_params(g, seed)), getattr(torch, dtype), emulate_bf16=bf16,
+                         order_seed=order_seed)
     pool = cycle or batch
     imgs = synth.fundus_batch(0, pool, res)
     labels = synth.labels(0, pool)
@@ -279,6 +281,23 @@ def main():
         curve["losses_bf16emu32"] = _net(299, 16, 0, steps=100, cycle=32, dtype="float32", bf16=True)["losses"]
         np.savez_compressed(p, **curve)
         print(f"curve16bf32: {time.time() - t0:.0f}s", flush=True)
+    for key, batch, cycle in (("curvecal4", 4, 8), ("curvecal16", 16, 32)):
+        if key not in todo:
+            continue
+        # K independent fp32 samples of the same 100 steps:
+        # each with its own fp32-exact summation order (permuted conv input
+        # channels and batch order, order seeds 1..K) and thread count; their
+        # spread around fp64 calibrates the fp32 curve test's bars
+        p = os.path.join(OUT, f"loss_curve_res299_b{batch}.npz")
+        curve = dict(np.load(p))
+        K = int(os.environ.get("CURVECAL_K", "6"))
+        threads = [8, 4, 2, 8, 6, 3, 8, 5][:K]
+        cal = [_net(299, batch, 0, steps=100, cycle=cycle, dtype="float32", order_seed=k + 1,
+                    threads=threads[k % len(threads)])["losses"] for k in range(K)]
+        curve["losses_fp32_cal"] = np.stack(cal)
+        curve["losses_fp32_cal_threads"] = np.array([threads[k % len(threads)] for k in range(K)])
+        np.savez_compressed(p, **curve)
+        print(f"{key}: {time.time() - t0:.0f}s", flush=True)
     if "eval299" in todo:
         eval299()
         print(f"eval299: {time.time() - t0:.0f}s", flush=True)

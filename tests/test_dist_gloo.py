@@ -60,7 +60,12 @@ def _worker(rank, world, port, q):
         before = ar.next
         ar.param_ready(off)
         issued.append(ar.next - before)
+    f_bwd = ar.fences
     scale = ar.finish()
+    # the lanes are fenced once per issue point that has a ready bucket, never
+    # at the other param_ready points (no per-conv join)
+    assert f_bwd == sum(1 for x in issued if x)
+    assert ar.fences - f_bwd in (0, 1) and ar.fences <= len(ar.buckets) < len(convs)
     q.put((rank, rep.grads.numpy() * scale, sum(1 for x in issued if x), len(ar.buckets)))
     dist.destroy_process_group()
 

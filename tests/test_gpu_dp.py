@@ -28,47 +28,59 @@ def _free_port():
     return p
 
 
-def _shard(step, rank):
+def _shard(step, rank, b=B, res=RES):
     from jr import synth
-    k = (step * WORLD + rank) * B
-    return synth.fundus_batch(k, B, RES), synth.labels(k, B, p=0.5)
+    k = (step * WORLD + rank) * b
+    return synth.fundus_batch(k, b, res), synth.labels(k, b, p=0.5)
 
 
-def _rank(rank, port, outdir, dtype="f32", payload="f32"):
+def _rank(rank, port, outdir, dtype="f32", payload="f32", b=B, res=RES, steps=STEPS):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     from jr.dist import BucketAllReduce
     from jr.engine import Engine
-    eng = Engine(B, RES, RES, seed=3, autotune=False, dtype=dtype)
+    eng = Engine(b, res, res, seed=3, autotune=False, dtype=dtype)
     ar = BucketAllReduce(eng, WORLD, bucket_bytes=8 << 20, payload=payload)
-    losses = []
-    for step in range(STEPS):
-        eng.set_batch(*_shard(step, rank))
+    losses, fences = [], []
+    for step in range(steps):
+        eng.set_batch(*_shard(step, rank, b, res))
         eng.train_step(allreduce=ar)
         losses.append(eng.loss_value())
+        fences.append(ar.fences)
         if step == 0:   # the reduced (summed) gradient of step 0
             np.save(os.path.join(outdir, f"grad{rank}.npy"), eng.grads.cpu().numpy())
     np.save(os.path.join(outdir, f"params{rank}.npy"), eng.params.cpu().numpy())
     np.save(os.path.join(outdir, f"losses{rank}.npy"), np.array(losses))
+    np.save(os.path.join(outdir, f"meta{rank}.npy"), np.array([len(ar.buckets), max(fences), eng.nlanes,
+                                                               int(eng.tiles == "pinned")]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype,payload", [("f32", "f32"), ("bf16", "f32"), ("bf16", "bf16")])
-def test_two_ranks_equal_one_process_averaging_shards(dtype, payload):
+# (dtype, payload, batch, resolution, steps): the 107^2 B=4 cases on the
+# planner's tiles, and the bench workload itself -- 299^2 B=64, two lanes, the
+# pinned MI355X tile tables (stream-K grids included) -- fp32 (x8) and bf16
+CASES = [("f32", "f32", B, RES, STEPS), ("bf16", "f32", B, RES, STEPS), ("bf16", "bf16", B, RES, STEPS),
+         ("f32", "f32", 64, 299, 2), ("bf16", "f32", 64, 299, 2)]
+
+
+@pytest.mark.parametrize("dtype,payload,b,res,steps", CASES)
+def test_two_ranks_equal_one_process_averaging_shards(dtype, payload, b, res, steps):
     """fp32 and bf16 engines (configs 2 and 3), fp32 or bf16 gradient payload.
     The one-process reference sums the two shards' gradients exactly as the
     two-rank all-reduce does: fp32 a + b, or (bf16 payload) each shard's
     gradient rounded to bf16, added, the sum rounded to bf16 (gloo / RCCL sum
-    bf16 values in fp32 -- exact for two terms -- and store bf16)."""
+    bf16 values in fp32 -- exact for two terms -- and store bf16).  The
+    buckets are issued from a stream that fences the lanes only at issue
+    points with a ready bucket (at most one fence per bucket per step)."""
     import torch.multiprocessing as mp
     from jr.engine import Engine
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.get_context("spawn")
-        ps = [ctx.Process(target=_rank, args=(r, port, d, dtype, payload)) for r in range(WORLD)]
+        ps = [ctx.Process(target=_rank, args=(r, port, d, dtype, payload, b, res, steps)) for r in range(WORLD)]
         for p in ps:
             p.start()
         for p in ps:
@@ -77,12 +89,16 @@ def test_two_ranks_equal_one_process_averaging_shards(dtype, payload):
         got = [np.load(os.path.join(d, f"params{r}.npy")) for r in range(WORLD)]
         got_losses = [np.load(os.path.join(d, f"losses{r}.npy")) for r in range(WORLD)]
         got_g0 = [np.load(os.path.join(d, f"grad{r}.npy")) for r in range(WORLD)]
-    ref = Engine(B, RES, RES, seed=3, autotune=False, dtype=dtype)
+        meta = [np.load(os.path.join(d, f"meta{r}.npy")) for r in range(WORLD)]
+    for nb, fences, nl, pinned in meta:
+        assert 1 <= fences <= nb and nl == 2
+        assert pinned == int(res == 299)            # the bench workload runs its committed tile table
+    ref = Engine(b, res, res, seed=3, autotune=False, dtype=dtype)
     ref_losses = [[], []]
-    for step in range(STEPS):
+    for step in range(steps):
         gsum = None
         for r in range(WORLD):
-            ref.set_batch(*_shard(step, r))
+            ref.set_batch(*_shard(step, r, b, res))
             ref.forward()
             ref.backward()
             ref.synchronize()
@@ -144,3 +160,49 @@ def test_jr_comm_rccl_world1(payload, tmp_path):
     b.synchronize()
     assert torch.equal(a.params, b.params)
     comm.close()
+
+
+def _world1_rccl(outdir, dtype):
+    """Child: a world-1 RCCL group (torch.distributed backend nccl) and the
+    bench workload's DP step (bench.py --dp on) next to the plain step."""
+    import socket as _s
+    sk = _s.socket()
+    sk.bind(("127.0.0.1", 0))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]), RANK="0", WORLD_SIZE="1")
+    sk.close()
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    from jr.dist import BucketAllReduce
+    from jr.engine import Engine
+    a = Engine(64, 299, 299, seed=3, dtype=dtype)
+    b = Engine(64, 299, 299, seed=3, dtype=dtype)
+    ar = BucketAllReduce(b, 1)
+    for step in range(2):
+        for e in (a, b):
+            e.set_batch(*_shard(step, 0, 64, 299))
+        a.train_step()
+        b.train_step(allreduce=ar)
+    a.synchronize()
+    b.synchronize()
+    np.save(os.path.join(outdir, "w1.npy"), np.array([int(torch.equal(a.params, b.params)), len(ar.buckets),
+                                                      ar.fences, int(a.tiles == "pinned")]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_world1_rccl_dp_step_equals_plain_step(dtype):
+    """The DP machinery at the bench workload (299^2 B=64, two lanes, pinned
+    tiles) over a real RCCL group of one rank: buckets issued from the feed
+    stream during the backward, lane 0 waiting for them only before the
+    optimizer -- bitwise the plain step, with at most one lane fence per
+    bucket."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        p = mp.get_context("spawn").Process(target=_world1_rccl, args=(d, dtype))
+        p.start()
+        p.join(600)
+        assert p.exitcode == 0, p.exitcode
+        same, nb, fences, pinned = np.load(os.path.join(d, "w1.npy"))
+    assert same == 1 and pinned == 1
+    assert 1 <= fences <= nb

@@ -3,9 +3,10 @@ id - 28, k_conv SK in csrc/jr_conv.hip) and JR_BF16 ids 33..57 (the stream-K
 grids of bf16 GEMM tiles 0..16 and wide tiles 0..7, k_conv_bf16 SK).
 
 A fixed grid of blocks walks equal ranges of the GEMM's tiles x K-tiles; a
-tile cut between blocks is finished by the block holding its first K-tile,
-which adds the later pieces' fp32 partials (published write-through, behind
-an agent-scope flag) in block order.  Checked here:
+tile cut between blocks is finished without any block waiting: every piece is
+published write-through and counted on its owner's word (agent-scope atomic),
+and the block whose count completes the tile adds the pieces in block order,
+the owner's first, and re-zeroes the word.  Checked here:
   * fwd (with the fused BN statistics), dgrad (every stride phase,
     accumulate) and wgrad against the fp64 oracle at the fp32 bars of
     test_gpu_ops.py (5e-6 / 1e-5 of max|ref|), on geometries whose tiles are
@@ -258,14 +259,18 @@ def test_stream_k_flags_reset_eager_and_graph():
 
 
 
+@pytest.mark.parametrize("poison", [1 << 20, 1, 2])
 @pytest.mark.parametrize("dtype,cfg", [(X8, SK0 + 11), (BF16, BF_SK0 + 0)])
-def test_stream_k_miscount_is_an_error_not_numbers(dtype, cfg):
-    """VERDICT r04 item 1b/1d, ADVICE r04: a stream-K hand-off that goes
+def test_stream_k_miscount_is_an_error_not_numbers(dtype, cfg, poison):
+    """VERDICT r04 item 1b/1d, ADVICE r04/r05: a stream-K hand-off that goes
     wrong must raise, never yield numbers.  Blocks no longer wait for one
     another (the block completing a tile's count finishes it), so the one
     device-side failure left is a count word not left zero: poisoned here
-    (jr_debug_poison_sk_counts), the launch counts the overrun into the
-    device error word and jr_device_check raises JR_ERR_DEVICE; the check
+    (jr_debug_poison_sk_counts).  A count past the piece count (1 << 20) is
+    counted into the device error word by the launch; a stale count BELOW
+    it (1, 2: a tile completes early and the word is left at the stale value
+    after the launch) is found by jr_device_check's scan of the idle
+    stream's words.  Either way jr_device_check raises JR_ERR_DEVICE and
     re-zeroes the words, so the next launches on the stream are bitwise the
     clean result again."""
     ffi = _lib()
@@ -293,7 +298,7 @@ def test_stream_k_miscount_is_an_error_not_numbers(dtype, cfg):
         fwd(ref)
         st_.synchronize()
         ffi.device_check()                        # a clean launch reports nothing
-        ffi.check("poison", L.jr_debug_poison_sk_counts(sp, 1 << 20))
+        ffi.check("poison", L.jr_debug_poison_sk_counts(sp, poison))
         Y = torch.zeros_like(ref)
         fwd(Y)
         st_.synchronize()
