@@ -80,8 +80,10 @@ def parse():
     ap.add_argument("--dp", default="auto", choices=["auto", "on", "off"],
                     help="bucketed gradient all-reduce in the step (jr.dist.BucketAllReduce): auto = only when "
                          "WORLD_SIZE > 1; on = also at N=1, over a world-1 RCCL group (the DP step timed on one GPU)")
-    ap.add_argument("--dp-transport", default="torch", choices=["torch", "jr"],
-                    help="torch.distributed all_reduce (backend nccl = RCCL) or libjr's own RCCL communicator")
+    ap.add_argument("--dp-transport", default="jr", choices=["torch", "jr"],
+                    help="libjr's own RCCL communicator (jr_comm_*, the default: measured +0.0 / +1.1 %% per fp32 / "
+                         "bf16 step over the plain step at N=1, vs +1.1 / +3.7 %% through torch.distributed, "
+                         "profiles/r06_dp_world1_ab.txt) or torch.distributed all_reduce (backend nccl = RCCL)")
     ap.add_argument("--no-defer-wgrad", action="store_true",
                     help="reduce each split-K filter gradient right after its GEMM (already the fp32 default; bf16 defers to one jr_wgrad_reduce)")
     return ap.parse_args()
@@ -494,12 +496,17 @@ def main():
     eng.set_batch(imgs, labels)
     eng.synchronize()
     log(f"engine ready (rank {rank}/{world})")
-    ar = None
+    ar = comm = None
+    transport = args.dp_transport
     if train and (world > 1 or args.dp == "on") and args.dp != "off":
-        comm = None
-        if args.dp_transport == "jr":
+        if transport == "jr":
+            from jr import _ffi
             from jr.dist import JrComm
-            comm = JrComm.from_torch_group(rank, world, local)
+            try:
+                comm = JrComm.from_torch_group(rank, world, local)
+            except _ffi.JRError as e:      # (the same RCCL under torch.distributed then)
+                log(f"libjr RCCL communicator unavailable ({e}); torch.distributed transport")
+                transport = "torch"
         ar = BucketAllReduce(eng, world, comm=comm)
     use_graph = False
 
@@ -526,6 +533,13 @@ def main():
     loss = eng.loss_value() if train else float(np.mean(eng.predictions()))
     if not np.isfinite(loss):
         raise SystemExit(f"non-finite {'loss' if train else 'prediction'} {loss}")
+    overlap = None
+    if ar is not None:          # after the timed region: one traced step (timing events per issue point)
+        ar.trace = True
+        step()
+        eng.synchronize()
+        overlap = ar.overlap_ms()
+        ar.trace = False
 
     devices = len({int(v) for v in gather_devices(dist, local)})
     rehearsal = world > 1 and (devices < world or dist.get_backend() != "nccl")
@@ -564,7 +578,8 @@ def main():
                                      {"transport": "jr_comm (RCCL)" if ar.comm is not None else
                                       f"torch.distributed {dist.get_backend()}", "buckets": len(ar.buckets),
                                       "payload": ar.payload, "fenced_issue_points_per_step": ar.fences,
-                                      "world": world}),
+                                      "world": world,
+                                      "issue_point_ready_ms_vs_backward_end": overlap}),
                        "tiles": eng.tiles,
                        "conv_math": CONV_MATH[args.conv_math] if args.dtype == "f32" else "bf16 MFMA"},
             ("final_loss" if train else "mean_prediction"): round(loss, 5),
@@ -578,6 +593,9 @@ def main():
         emit(json_fd, out)
     if dist:
         dist.barrier()
+        if comm is not None:
+            torch.cuda.synchronize()
+            comm.close()
         dist.destroy_process_group()
 
 

@@ -173,11 +173,35 @@ class BucketAllReduce:
         self.feed = (torch.cuda.Stream(device=engine.grads.device)
                      if comm is None and getattr(engine, "stream", None) is not None else None)
         self.fences = 0                 # issue points that fenced the lanes (one per issue point with work)
+        # trace=True: timing events on the issuing stream right after each
+        # fence (the bucket's gradients are final: its all-reduce can start)
+        # and on lane 0 when the backward has been joined (finish); see
+        # overlap_ms()
+        self.trace = False
+        self._tev: List[Tuple[str, object]] = []
 
     def begin(self, eng=None) -> None:
         self.works = []
         self.next = 0
         self.fences = 0
+        self._tev = []
+
+    def _mark(self, kind: str, stream) -> None:
+        if self.trace and stream is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+            self._tev.append((kind, ev))
+
+    def overlap_ms(self) -> List[float]:
+        """After a traced step (trace=True) has completed: for each issue
+        point, when its buckets could start relative to the end of the
+        backward, in ms (negative: while the backward was still running --
+        the all-reduce overlaps it)."""
+        end = next((ev for k, ev in self._tev if k == "backward_end"), None)
+        if end is None:
+            return []
+        end.synchronize()
+        return [round(end.elapsed_time(ev), 3) for k, ev in self._tev if k == "ready"]
 
     def _stream_ctx(self):
         s = getattr(self.eng, "stream", None)
@@ -232,7 +256,9 @@ class BucketAllReduce:
     def _issue_ready(self, ready_from: int) -> None:
         if not self.ready(ready_from):
             return                      # nothing to issue: no fence, no wait anywhere
-        self._fence(self.comm_stream if self.comm is not None else self.feed)
+        st = self.comm_stream if self.comm is not None else self.feed
+        self._fence(st)
+        self._mark("ready", st)
         while self.ready(ready_from):
             lo, hi = self.buckets[self.next]
             if self.comm is not None:
@@ -247,6 +273,7 @@ class BucketAllReduce:
         self._issue_ready(offset)
 
     def finish(self, eng=None) -> float:
+        self._mark("backward_end", getattr(self.eng, "stream", None))
         self._issue_ready(0)
         if self.comm is not None:
             self._done_ev.record(self.comm_stream)

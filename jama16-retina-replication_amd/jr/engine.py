@@ -149,6 +149,7 @@ class Engine:
         # event recorded right after it) instead of the other lane's tail
         # (JR_PRECISE_WAITS=0: tail waits, as captured graphs always use)
         self.precise_waits = os.environ.get("JR_PRECISE_WAITS", "1") != "0"
+        self._join_each = os.environ.get("JR_DP_JOIN_EACH", "0") == "1"
         self._prod_ev: Dict[int, object] = {}
         # producer events: libjr's (no timing, no system-scope fence: cheaper
         # to record) or torch's (JR_LANE_EVENTS=torch, for A/B runs)
@@ -979,6 +980,8 @@ class Engine:
                 # only when a bucket is actually issued (fence_lanes); lane 0
                 # never waits for lane 1 at a conv unit
                 if hook is not None:
+                    if self._join_each:     # round-5 behaviour, A/B runs only (JR_DP_JOIN_EACH=1)
+                        self._join()
                     hook(c.args)
                 continue
             st = self.lane_streams[c.lane]

@@ -12,11 +12,12 @@ out=gpurun_out/dp
 mkdir -p $out
 for r in $(seq 1 $rounds); do
   for dt in f32 bf16; do
-    for dp in off torch jr; do
-      a="--dp off"
+    for dp in off torch jr joineach; do
+      a="--dp off"; env=""
       [ $dp = torch ] && a="--dp on --dp-transport torch"
       [ $dp = jr ] && a="--dp on --dp-transport jr"
-      timeout -k 10 240 python bench.py --steps $steps --warmup 10 --no-cpu-baseline --no-roofline --dtype $dt $a \
+      [ $dp = joineach ] && a="--dp on --dp-transport torch" && env="JR_DP_JOIN_EACH=1"
+      env $env timeout -k 10 240 python bench.py --steps $steps --warmup 10 --no-cpu-baseline --no-roofline --dtype $dt $a \
         > $out/line_${dt}_${dp}_$r.json 2> $out/line_${dt}_${dp}_$r.log
       python -c "import json;d=json.load(open('$out/line_${dt}_${dp}_$r.json'));print('$dt $dp round $r', d['ms_per_step'], 'ms', d['config'].get('allreduce'))"
     done
