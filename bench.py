@@ -472,9 +472,24 @@ def emit(fd: int, out: dict) -> None:
     os.write(fd, (json.dumps(out) + "\n").encode())
 
 
+def heartbeat(period: float = 50.0) -> None:
+    """A progress line on stderr every `period` s from a daemon thread: long
+    single passes (the 57,000-image ensemble in fp32 runs minutes between
+    log lines) must not look hung to a watchdog."""
+    import threading
+    t0 = time.perf_counter()
+
+    def run():
+        while True:
+            time.sleep(period)
+            log(f"alive, {time.perf_counter() - t0:.0f} s")
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     args = parse()
     json_fd = _stdout_for_json_only()
+    heartbeat()
     if args.mode == "ensemble":
         out = ensemble_bench(args)
         if out is not None:

@@ -112,6 +112,11 @@ int jr_device_check(void);
  * current device's) to `value`, in stream order -- the next stream-K launch
  * there then miscounts and must be reported by jr_device_check. */
 int jr_debug_poison_sk_counts(void* stream, uint32_t value);
+/* Diagnostics (probe): while `on`, JR_F32_X8 GEMMs on non-stream-K tiles run
+ * a fp16 three-way split with six f16 MFMAs per product, the A / B operands
+ * scaled by sa / sb (powers of two putting max |x| below 2^15) and the
+ * result by 1 / (sa sb).  Process-wide, not for production use. */
+int jr_debug_x8_f16(int on, float sa, float sb);
 
 /* ---- convolution (train.py:129-130 -> Keras Conv2D -> TF Conv2D,
  *      Conv2DBackpropInput, Conv2DBackpropFilter created by .minimize at

@@ -120,6 +120,58 @@ struct SplitFrag {
   __device__ __forceinline__ bf16x8 l() const { return __builtin_bit_cast(bf16x8, (u32x4){lp[0], lp[1], lp[2], lp[3]}); }
 };
 
+// H6 probe (jr_debug_x8_f16): the same three-way split
+// into fp16 (11-bit significands) of the operand scaled by a power of two
+// (so its largest magnitude sits in [2^14, 2^15)): x s = h + m + l with h =
+// rtz(x s), m = rtz(x s - h), l = x s - h - m -- every remainder exact in
+// fp32 (a truncation's tail), l at most 2 bits, exact while x s >= 2^-1
+// (fp16 subnormals keep the rest down to 2^-24).  Six f16 MFMAs per
+// product (hh hm mh mm hl lh); dropped: ml + lm (< 2^-32 |a b|) and ll, the
+// x8 class.  acc is scaled back by 2^-(ka+kb) (exact) after the K loop.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pkrtz_f16(float a, float b) {   // v_cvt_pkrtz_f16_f32, a in the low half
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+}
+
+struct SplitFrag16 {
+  float x[8];
+  uint32_t hp[4], mp[4], lp[4];
+  __device__ __forceinline__ void init(const float* v, float scale) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) x[t] = v[t] * scale;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) hp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
+  }
+  __device__ __forceinline__ static float lo(uint32_t u) {
+    return (float)__builtin_bit_cast(f16x2, u)[0];
+  }
+  __device__ __forceinline__ static float hi(uint32_t u) {
+    return (float)__builtin_bit_cast(f16x2, u)[1];
+  }
+  __device__ __forceinline__ void stage2() {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      x[2 * p] = sub_f32(x[2 * p], lo(hp[p]));
+      x[2 * p + 1] = sub_f32(x[2 * p + 1], hi(hp[p]));
+      mp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
+    }
+  }
+  __device__ __forceinline__ void stage3() {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      x[2 * p] = sub_f32(x[2 * p], lo(mp[p]));
+      x[2 * p + 1] = sub_f32(x[2 * p + 1], hi(mp[p]));
+      lp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
+    }
+  }
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  __device__ __forceinline__ f16x8 h() const { return __builtin_bit_cast(f16x8, (u32x4){hp[0], hp[1], hp[2], hp[3]}); }
+  __device__ __forceinline__ f16x8 m() const { return __builtin_bit_cast(f16x8, (u32x4){mp[0], mp[1], mp[2], mp[3]}); }
+  __device__ __forceinline__ f16x8 l() const { return __builtin_bit_cast(f16x8, (u32x4){lp[0], lp[1], lp[2], lp[3]}); }
+};
+
 // DBG (diagnostic builds only, jr_conv2d_debug_time): 1 = no MFMA,
 // 2 = no DMA after the first tile (results are wrong in both).
 //
@@ -148,7 +200,8 @@ struct SplitFrag {
 // so concurrent kernels on other lanes or processes cannot stall a grid.  The
 // count words are per-stream library words (stream_scratch) that the
 // completing block resets, so a launch needs no memset.
-template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0, bool SK = false>
+template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0, bool SK = false,
+          bool H6 = false>
 __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int WGN = 4 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -548,6 +601,63 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc[i][j], 0, 0, 0);
         }
       };
+      if constexpr (H6) {
+        auto mmh = [&](int i, int j, const f16x8& x, const f16x8& y) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(x, y, acc[i][j], 0, 0, 0);
+        };
+#pragma unroll
+        for (int g8 = 0; g8 < G8; ++g8) {
+          SplitFrag16 sa[TM], sb[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) sa[i].init(&af[i][8 * g8], g.h_sa);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) sb[j].init(&bfr[j][8 * g8], g.h_sb);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) mmh(i, j, sa[i].h(), sb[j].h());
+#pragma unroll
+          for (int i = 0; i < TM; ++i) sa[i].stage2();
+          next_piece();
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) mmh(i, j, sa[i].m(), sb[j].h());
+#pragma unroll
+          for (int j = 0; j < TN; ++j) sb[j].stage2();
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              mmh(i, j, sa[i].h(), sb[j].m());
+              mmh(i, j, sa[i].m(), sb[j].m());
+            }
+#pragma unroll
+          for (int i = 0; i < TM; ++i) sa[i].stage3();
+          next_piece();
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) mmh(i, j, sa[i].l(), sb[j].h());
+#pragma unroll
+          for (int j = 0; j < TN; ++j) sb[j].stage3();
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) mmh(i, j, sa[i].h(), sb[j].l());
+          next_piece();
+        }
+        if constexpr (DO_ISSUE && DBG != 2) {
+#pragma unroll
+          for (int d = 3 * G8; d < NPIECE; ++d) issue_piece(kt + NBUF - 1, d, wA, wB);
+          advance();
+        }
+        return;
+      }
 #pragma unroll
       for (int g8 = 0; g8 < G8; ++g8) {
         SplitFrag sa[TM], sb[TN];
@@ -670,6 +780,14 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     }
   }
   JR_ST(stamp.loop();)
+  if constexpr (H6) {        // back from the operands' power-of-two scales (exact)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] *= g.h_unscale;
+  }
 
   if constexpr (SK) {
     sk_first = false;
@@ -804,15 +922,25 @@ constexpr int kSkMinIters = 4;     // K-tiles per stream-K block at least
 // (the fp32 engine default), and fewer slabs measured 0.12-0.14 ms per step
 // faster on two boxes (profiles/r05_ab_wsplit*_f32.txt; 320 / 1,024 slower,
 // bf16 at 384 slower). JR_WGRAD_SPLIT_TARGET overrides it (A/B knob, read once).
-static int split_target(int dtype, int op) {
+// JR_WGRAD_SPLIT_KMAX (A/B knob, read once): x8 filter gradients aim for 384
+// only where K = B.Ho.Wo is at most this, 640 above it (round 5's
+// K-bounded rule: faster at 299^2 and 587^2, moved the B=16 fp32 curve
+// past the round-5 bar; re-judged against the calibrated bars).
+static int split_target(int dtype, int op, long long K) {
   static const int wg = [] {
     const char* e = std::getenv("JR_WGRAD_SPLIT_TARGET");
     const int v = e ? std::atoi(e) : 0;
     return v > 0 ? v : 0;
   }();
+  static const long long kmax = [] {
+    const char* e = std::getenv("JR_WGRAD_SPLIT_KMAX");
+    const long long v = e ? std::atoll(e) : 0;
+    return v > 0 ? v : 0LL;
+  }();
   if (op != OP_WGRAD) return 640;
   if (wg > 0) return wg;
-  return dtype == JR_F32_X8 || dtype == JR_F32_X8P ? 384 : 640;
+  if (dtype == JR_F32_X8 || dtype == JR_F32_X8P) return kmax > 0 && K > kmax ? 640 : 384;
+  return 640;
 }
 
 static Plan plan_with(int dtype, int cfg, int M, int N, int K, int op) {
@@ -824,7 +952,7 @@ static Plan plan_with(int dtype, int cfg, int M, int N, int K, int op) {
   p.ktiles = (int)ceil_div(K, t.bk);
   const int tiles = p.mt * p.nt;
   int splits = 1;
-  const int target = split_target(dtype, op);
+  const int target = split_target(dtype, op, K);
   if (tiles < target) {
     splits = (int)ceil_div(target, tiles);
     const int max_by_k = std::max(1, p.ktiles / 8);
@@ -955,37 +1083,47 @@ static size_t stats_ws(int dtype, const Plan& p) {
 // Fast-path kernels (UT): FWD/DGRAD when the reduction channel radix is a
 // multiple of BK (every layer but conv1 FWD at BK = 16); WGRAD when BK / wo < ho
 // (one carry per radix and K-tile: the incremental pixel walk).
-template <int OP, int C, int DBG, bool X8, bool SK>
+template <int OP, int C, int DBG, bool X8, bool SK, bool H6 = false>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t s) {
   constexpr TileCfg t = kCfgs[C];
   const bool fast = OP == OP_WGRAD ? t.bk / a.wo < a.ho : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
   if (fast) {
-    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, X8, DBG, SK>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, X8, DBG, SK, H6>), grid, dim3(256), 0, s, a);
     return;
   }
   if constexpr (DBG == 0)
-    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, X8, 0, SK>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, false, X8, 0, SK, H6>), grid, dim3(256), 0, s, a);
 }
 
 // SK: the stream-K grid (k_conv SK) of the tile
-template <int OP, int DBG = 0, bool X8 = false, bool SK = false>
+template <int OP, int DBG = 0, bool X8 = false, bool SK = false, bool H6 = false>
 static void launch_op(int cfg, const ConvArgs& a, dim3 grid, hipStream_t s) {
   switch (cfg) {
-    case 0: launch_cfg<OP, 0, DBG, X8, SK>(a, grid, s); break;
-    case 1: launch_cfg<OP, 1, DBG, X8, SK>(a, grid, s); break;
-    case 2: launch_cfg<OP, 2, DBG, X8, SK>(a, grid, s); break;
-    case 3: launch_cfg<OP, 3, DBG, X8, SK>(a, grid, s); break;
-    case 4: launch_cfg<OP, 4, DBG, X8, SK>(a, grid, s); break;
-    case 5: launch_cfg<OP, 5, DBG, X8, SK>(a, grid, s); break;
-    case 6: launch_cfg<OP, 6, DBG, X8, SK>(a, grid, s); break;
-    case 7: launch_cfg<OP, 7, DBG, X8, SK>(a, grid, s); break;
-    case 8: launch_cfg<OP, 8, DBG, X8, SK>(a, grid, s); break;
-    case 9: launch_cfg<OP, 9, DBG, X8, SK>(a, grid, s); break;
-    case 10: launch_cfg<OP, 10, DBG, X8, SK>(a, grid, s); break;
-    case 11: launch_cfg<OP, 11, DBG, X8, SK>(a, grid, s); break;
-    case 12: launch_cfg<OP, 12, DBG, X8, SK>(a, grid, s); break;
-    default: launch_cfg<OP, 13, DBG, X8, SK>(a, grid, s); break;
+    case 0: launch_cfg<OP, 0, DBG, X8, SK, H6>(a, grid, s); break;
+    case 1: launch_cfg<OP, 1, DBG, X8, SK, H6>(a, grid, s); break;
+    case 2: launch_cfg<OP, 2, DBG, X8, SK, H6>(a, grid, s); break;
+    case 3: launch_cfg<OP, 3, DBG, X8, SK, H6>(a, grid, s); break;
+    case 4: launch_cfg<OP, 4, DBG, X8, SK, H6>(a, grid, s); break;
+    case 5: launch_cfg<OP, 5, DBG, X8, SK, H6>(a, grid, s); break;
+    case 6: launch_cfg<OP, 6, DBG, X8, SK, H6>(a, grid, s); break;
+    case 7: launch_cfg<OP, 7, DBG, X8, SK, H6>(a, grid, s); break;
+    case 8: launch_cfg<OP, 8, DBG, X8, SK, H6>(a, grid, s); break;
+    case 9: launch_cfg<OP, 9, DBG, X8, SK, H6>(a, grid, s); break;
+    case 10: launch_cfg<OP, 10, DBG, X8, SK, H6>(a, grid, s); break;
+    case 11: launch_cfg<OP, 11, DBG, X8, SK, H6>(a, grid, s); break;
+    case 12: launch_cfg<OP, 12, DBG, X8, SK, H6>(a, grid, s); break;
+    default: launch_cfg<OP, 13, DBG, X8, SK, H6>(a, grid, s); break;
   }
+}
+
+// H6 probe switch (jr_debug_x8_f16): JR_F32_X8 launches of the non-stream-K
+// tiles run the fp16 six-product kernel with these operand scales
+static struct { int on; float sa, sb; } g_x6h = {0, 1.f, 1.f};
+JR_API int jr_debug_x8_f16(int on, float sa, float sb) {
+  g_x6h.on = on;
+  g_x6h.sa = sa;
+  g_x6h.sb = sb;
+  return JR_OK;
 }
 
 static int validate(const jr_conv_desc* d, int op, int dtype) {
@@ -1184,6 +1322,11 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     launch_op<OP>(p.tile - kNumCfgs, a, grid, s);     // the fp32-MFMA kernel of that tile
   } else if (p.sk) {
     launch_op<OP, 0, true, true>(p.tile - 2 * kNumCfgs, a, grid, s);   // the stream-K grid of that x8 tile
+  } else if (dtype == JR_F32_X8 && g_x6h.on) {
+    a.h_sa = g_x6h.sa;
+    a.h_sb = g_x6h.sb;
+    a.h_unscale = 1.f / (g_x6h.sa * g_x6h.sb);
+    launch_op<OP, 0, true, false, true>(p.tile, a, grid, s);
   } else if (dtype == JR_F32_X8) {
     launch_op<OP, 0, true>(p.tile, a, grid, s);
   } else {

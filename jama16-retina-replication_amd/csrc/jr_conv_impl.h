@@ -56,6 +56,8 @@ struct ConvArgs {
   float* sk_part;
   // the library's device error word (jr_device_check)
   unsigned* sk_err;
+  // fp16 six-product probe (jr_debug_x8_f16): operand scales, 1 / (sa sb)
+  float h_sa, h_sb, h_unscale;
 };
 
 // Moves a grouped GEMM's operand / output pointers to member blockIdx.y

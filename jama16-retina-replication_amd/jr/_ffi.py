@@ -198,6 +198,7 @@ _SIGS = {
     "jr_event_destroy": (c_int, [c_void_p]),
     "jr_device_check": (c_int, []),
     "jr_debug_poison_sk_counts": (c_int, [c_void_p, ctypes.c_uint32]),
+    "jr_debug_x8_f16": (c_int, [c_int, ctypes.c_float, ctypes.c_float]),
 }
 
 EXPORTED = tuple(_SIGS)

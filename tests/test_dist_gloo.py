@@ -40,6 +40,7 @@ def test_buckets_cover_flat_gradient_in_reverse_order():
     starts = {off for _, _, off, _ in layout}
     assert all(lo in starts for lo, _ in b)                 # cut at tensor starts
     assert 3 <= len(b) <= 6                                 # ~87 MB / 24 MB
+    assert 4 * (b[-1][1] - b[-1][0]) <= 2 << 20             # the unhidden last bucket kept small
 
 
 def _worker(rank, world, port, q):
