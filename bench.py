@@ -33,12 +33,15 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 # MI355X dense MFMA (MI355X_MICROARCH.md); x8 = eight bf16 MFMAs per fp32 product
-PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0, "x8": round(2500.0 / 8, 1), "x8p": round(2500.0 / 8, 1)}
+PEAK_TFLOPS = {"f32": 157.3, "bf16": 2500.0, "x8": round(2500.0 / 8, 1), "x8p": round(2500.0 / 8, 1),
+               "x6h": round(2500.0 / 6, 1)}
 CONV_MATH = {"f32": "fp32 MFMA (v_mfma_f32_32x32x2_f32)",
              "x8": "fp32 via exact 3-way bf16 split, 8 bf16 MFMAs per product (all terms > 2^-32), "
                    "fp32 accumulate (JR_F32_X8)",
              "x8p": "fp32 via exact 3-way bf16 split done once per operand (jr_split_x8p planes), 8 bf16 MFMAs "
-                    "per product, fp32 accumulate (JR_F32_X8P)"}
+                    "per product, fp32 accumulate (JR_F32_X8P)",
+             "x6h": "fp32 via a power-of-two-scaled 3-way fp16 split, 6 f16 MFMAs per product (dropped terms < "
+                    "2^-32), fp32 accumulate (JR_F32_X6H)"}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -62,7 +65,7 @@ def parse():
                     help="ensemble mode: one engine per member instead of the grouped EnsembleEngine")
     ap.add_argument("--res", type=int, default=299)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
-    ap.add_argument("--conv-math", default="x8", choices=["f32", "x8", "x8p"],
+    ap.add_argument("--conv-math", default="x8", choices=["f32", "x8", "x8p", "x6h"],
                     help="dtype f32 only. x8 (default): fp32 tensors, products from an exact 3-way bf16 split "
                          "(jr.h JR_F32_X8, fp32-accurate); f32: fp32 MFMA")
     # eager launches on two lanes only: round 2 measured them 1.3-1.5 % faster

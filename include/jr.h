@@ -42,6 +42,17 @@
  *    n*ho*wo*y_c_stride (dy), c_out*kh*kw*c8 (W^T), kh*kw*c_in*c_out (HWIO).
  *    Eight MFMAs per product in the JR_F32_X8 order; outputs (y, dx, dw) are
  *    fp32 exactly as for JR_F32.
+ *    JR_F32_X6H (convolution entry points only) = fp32 tensors as JR_F32_X8,
+ *    the products on the fp16 matrix cores: each operand is scaled by a
+ *    power of two s that puts its largest magnitude (the descriptor's
+ *    x/w/dy absmax or bound) in [2^14, 2^15) and split into three fp16 terms
+ *    x s = h + m + l (11-bit significands: exact for |x s| >= 2^-1, i.e.
+ *    down to 2^-15 of the tensor's max, and down to 2^-24 absolute through
+ *    fp16 subnormals); six f16 MFMAs accumulate hh+hm+mh+mm+hl+lh in fp32
+ *    (dropped: ml + lm < 2^-32 |a b| and l*l, the JR_F32_X8 class), and the
+ *    result is scaled back exactly.  Same tiles, config ids, split-K and
+ *    stream-K plans as JR_F32_X8; 3/4 of its MFMAs.  A magnitude above the
+ *    stated bound saturates (wrong results): bounds must hold.
  */
 #ifndef JR_H_
 #define JR_H_
@@ -62,7 +73,7 @@ typedef enum jr_status {
   JR_ERR_DEVICE = -5       /* a kernel reported a device-side failure      */
 } jr_status;
 
-typedef enum jr_dtype { JR_F32 = 0, JR_BF16 = 1, JR_F32_X8 = 2, JR_F32_X8P = 3 } jr_dtype;
+typedef enum jr_dtype { JR_F32 = 0, JR_BF16 = 1, JR_F32_X8 = 2, JR_F32_X8P = 3, JR_F32_X6H = 4 } jr_dtype;
 
 typedef enum jr_conv_op { JR_CONV_FWD = 0, JR_CONV_BWD_DATA = 1, JR_CONV_BWD_FILTER = 2 } jr_conv_op;
 
@@ -79,6 +90,16 @@ typedef struct jr_conv_desc {
   int32_t ho, wo;                 /* output [n, ho, wo, c_out] (slice)     */
   int32_t x_c_off, x_c_stride;    /* channel slice of the input buffer     */
   int32_t y_c_off, y_c_stride;    /* channel slice of the output buffer    */
+  /* JR_F32_X6H only (ignored by every other dtype; zero-initialise): the
+   * largest magnitude of x, of the filter block w and of dy, which set each
+   * operand's power-of-two scale.  *_absmax: NULL, or 64 device floats whose
+   * maximum is (an upper bound of) max |tensor| -- jr_absmax_prep for
+   * filters, jr_bn_relu_bwd_multi_absmax / jr_bn_relu_bwd_maxpool_absmax for
+   * a data gradient; when NULL, *_bound is a host upper bound (0: 2^14). */
+  const float* x_absmax;
+  const float* w_absmax;
+  const float* dy_absmax;
+  float x_bound, w_bound, dy_bound;
 } jr_conv_desc;
 
 /* 3x3 pooling window; max: stride 2 'valid', avg: stride 1 'same' with the
@@ -112,11 +133,7 @@ int jr_device_check(void);
  * current device's) to `value`, in stream order -- the next stream-K launch
  * there then miscounts and must be reported by jr_device_check. */
 int jr_debug_poison_sk_counts(void* stream, uint32_t value);
-/* Diagnostics (probe): while `on`, JR_F32_X8 GEMMs on non-stream-K tiles run
- * a fp16 three-way split with six f16 MFMAs per product, the A / B operands
- * scaled by sa / sb (powers of two putting max |x| below 2^15) and the
- * result by 1 / (sa sb).  Process-wide, not for production use. */
-int jr_debug_x8_f16(int on, float sa, float sb);
+
 
 /* ---- convolution (train.py:129-130 -> Keras Conv2D -> TF Conv2D,
  *      Conv2DBackpropInput, Conv2DBackpropFilter created by .minimize at
@@ -291,6 +308,13 @@ typedef struct jr_bn_seg {
 int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
                          int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd, void* dx,
                          void* ws, size_t ws_bytes, void* stream);
+/* jr_bn_relu_bwd_multi that also raises dx_absmax (64 device floats the
+ * caller zeroed before the first launch that feeds them) so that their max
+ * is max |dx| of every launch that fed them: the dy_absmax of the
+ * JR_F32_X6H data- / filter-gradient GEMMs reading dx. */
+int jr_bn_relu_bwd_multi_absmax(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
+                                int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd,
+                                void* dx, void* ws, size_t ws_bytes, float* dx_absmax, void* stream);
 /* Up to 8 independent conv2d_bn backwards (the branch-final layers of one
  * Inception block, whose upstream gradients become final together) in ONE
  * set of three launches; layer l is exactly the jr_bn_relu_bwd_multi call
@@ -323,6 +347,11 @@ size_t jr_bn_relu_bwd_maxpool_workspace_size(const jr_pool_desc* d);
 int jr_bn_relu_bwd_maxpool(int dtype, const jr_pool_desc* d, const uint8_t* argmax, const void* pooled_dy, void* dy,
                            const void* x, int32_t x_c_stride, const float* mean, const float* invstd,
                            const float* beta, void* dx, float* dbeta, void* ws, size_t ws_bytes, void* stream);
+/* ... raising dx_absmax as jr_bn_relu_bwd_multi_absmax does. */
+int jr_bn_relu_bwd_maxpool_absmax(int dtype, const jr_pool_desc* d, const uint8_t* argmax, const void* pooled_dy,
+                                  void* dy, const void* x, int32_t x_c_stride, const float* mean, const float* invstd,
+                                  const float* beta, void* dx, float* dbeta, void* ws, size_t ws_bytes,
+                                  float* dx_absmax, void* stream);
 
 /* ---- pooling (Keras MaxPooling2D((3,3),(2,2)) / AveragePooling2D((3,3),
  *      (1,1),'same') inside InceptionV3, train.py:129-130) ------------ */
@@ -413,6 +442,22 @@ int jr_conv_weights_x8p_multi(const jr_wprep* layers, int32_t n_layers, int32_t 
  * zeros (the conv1 image: c = 3, c_pad = 8). */
 int jr_split_x8p(const float* src, int64_t rows, int32_t c, int32_t src_off, int32_t src_stride, void* dst,
                  int32_t c_pad, int32_t dst_off, int32_t dst_stride, int64_t plane_stride, void* stream);
+
+/* JR_F32_X6H operand magnitudes of parameter blocks (once per step, before
+ * the forward): out[0 .. zero_floats) is zeroed (in stream order), then for
+ * each segment the 64 floats out[seg.out * 64 ...] are raised so that their
+ * max is max |src[off .. off + count)| (a conv launch's filter block: its
+ * w_absmax).  limit > 0: a max above it counts a failure into the
+ * device error word, which jr_device_check reports (JR_ERR_DEVICE) -- the
+ * guard of a host bound that rests on these values (the BN betas bound the
+ * activations: |relu(xhat + beta)| <= sqrt(N - 1) + max |beta|). */
+typedef struct jr_absmax_seg {
+  int64_t off, count;
+  int32_t out;
+  float limit;
+} jr_absmax_seg;
+int jr_absmax_prep(const float* src, const jr_absmax_seg* segs, int32_t nseg, float* out, int64_t zero_floats,
+                   void* stream);
 
 /* ---- dtype helpers --------------------------------------------------- */
 int jr_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream);

@@ -182,10 +182,12 @@ JR_API int jr_device_check(void) {
   }
   (void)hipMemset(w, 0, sizeof(unsigned));
   (void)hipDeviceSynchronize();
-  return fail(JR_ERR_DEVICE, "stream-K hand-off: " + std::to_string(h) +
-                                 " count(s) found past their tile's piece count and " + std::to_string(stale) +
-                                 " hand-off word(s) of idle streams not left zero; the outputs of the launches since "
-                                 "the last jr_device_check are invalid (hand-off words reset)");
+  return fail(JR_ERR_DEVICE, "device check: " + std::to_string(h) +
+                                 " failure(s) counted by kernels (a stream-K hand-off count past its tile's piece "
+                                 "count, or a JR_F32_X6H magnitude bound exceeded: jr_absmax_prep) and " +
+                                 std::to_string(stale) +
+                                 " stream-K hand-off word(s) of idle streams not left zero; the outputs of the "
+                                 "launches since the last jr_device_check are invalid (hand-off words reset)");
 }
 
 JR_API int jr_debug_poison_sk_counts(void* stream, uint32_t value) {

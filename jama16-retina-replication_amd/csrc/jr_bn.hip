@@ -144,6 +144,9 @@ struct BnSegs {
   int dy_off[kMaxSegs], dy_stride[kMaxSegs];
   int c0[kMaxSegs + 1];   // first channel of each segment; c0[n] = c
   int n;
+  // backward apply: NULL, or 64 words that receive max |dx| (atomicMax on the
+  // bits of each block's max into word blockIdx.x % 64; JR_F32_X6H scales)
+  float* absmax;
 };
 
 __device__ __forceinline__ int seg_of(const BnSegs& sg, int ch) {
@@ -527,17 +530,18 @@ __global__ void __launch_bounds__(256) k_bn_relu_apply_stats(const T* __restrict
   }
 }
 
+// returns the largest |dx| this thread stored (0 if none)
 template <typename T>
-__device__ __forceinline__ void bn_bwd_apply_body(const BnSegs& sg, const T* __restrict__ x, int xs, int64_t m, int c,
-                                                  const float* __restrict__ mean, const float* __restrict__ invstd,
-                                                  const float* __restrict__ k1, const float* __restrict__ k2, T* dx,
-                                                  int bx) {
+__device__ __forceinline__ float bn_bwd_apply_body(const BnSegs& sg, const T* __restrict__ x, int xs, int64_t m, int c,
+                                                   const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                   const float* __restrict__ k1, const float* __restrict__ k2, T* dx,
+                                                   int bx) {
   constexpr int VW = Vec<T>::N;
   const int tpr = c / VW;
   const int rpp = 256 / tpr;
   const int t = threadIdx.x;
   const int q = t % tpr, rr = t / tpr;
-  if (rr >= rpp) return;
+  if (rr >= rpp) return 0.f;
   const int sgi = seg_of(sg, q * VW), lc = q * VW - sg.c0[sgi];
   const T* dy = static_cast<const T*>(sg.dy[sgi]) + sg.dy_off[sgi] + lc;
   const int dy_stride = sg.dy_stride[sgi];
@@ -562,6 +566,7 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnSegs& sg, const T* __r
     pin(xr[u]);
     pin(gr[u]);
   }
+  float amax = 0.f;
 #pragma unroll
   for (int u = 0; u < kAppUnroll; ++u) {
     const int64_t r = r0 + (int64_t)u * rpp;
@@ -575,8 +580,25 @@ __device__ __forceinline__ void bn_bwd_apply_body(const BnSegs& sg, const T* __r
       const float pre = __fadd_rn(xh, be[j]);
       const float g = pre > 0.f ? gv[j] : 0.f;
       o[j] = is[j] * (g - c1[j] - xh * c2[j]);
+      amax = fmaxf(amax, fabsf(o[j]));
     }
     Vec<T>::st(dx + r * xs + q * VW, o);
+  }
+  return amax;
+}
+
+// The block's max of v into word blockIdx.x % 64 of out (atomicMax on the
+// float bits: every value is >= 0).  Every thread of the block calls it.
+__device__ __forceinline__ void block_absmax_to(float v, float* out) {
+  __shared__ float s_max[4];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = s_max[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) b = fmaxf(b, s_max[w]);
+    atomicMax(reinterpret_cast<unsigned*>(out) + (blockIdx.x & 63), __float_as_uint(b));
   }
 }
 
@@ -586,7 +608,8 @@ __global__ void __launch_bounds__(256) k_bn_relu_bwd_apply(BnSegs sg, const T* _
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ k1,
                                                            const float* __restrict__ k2, T* dx) {
-  bn_bwd_apply_body<T>(sg, x, xs, m, c, mean, invstd, k1, k2, dx, blockIdx.x);
+  const float amax = bn_bwd_apply_body<T>(sg, x, xs, m, c, mean, invstd, k1, k2, dx, blockIdx.x);
+  if (sg.absmax) block_absmax_to(amax, sg.absmax);   // (uniform: a kernel argument)
 }
 
 // Canonical combine of ONE channel's backward-reduce partials when there are
@@ -985,7 +1008,7 @@ static int bn_bwd_launch(int dtype, const BnSegs& sg, const void* x, int32_t x_c
   int rc = check_launch("bn_bwd reduce");
   if (rc) return rc;
   if (g.nchunks <= kFoldMaxP) {
-    if (fold_bwd()) {   // the finalize inside the apply: one kernel boundary fewer
+    if (fold_bwd() && !sg.absmax) {   // the finalize inside the apply: one kernel boundary fewer
       const int vw = vec_width(dtype);
       const int step = 256 / (kFoldCh / vw) * kAppUnroll;
       const int rpb = (int)std::max<int64_t>(step, (int64_t)(fold_rows() + step - 1) / step * step);
@@ -1054,9 +1077,18 @@ static int bwd_setup(int dtype, int nseg, const jr_bn_seg* segs, const void*& x,
 JR_API int jr_bn_relu_bwd_multi(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
                                 int32_t x_c_stride, int64_t m, int32_t c, const float* mean, const float* invstd,
                                 void* dx, void* ws, size_t ws_bytes, void* stream) {
+  return jr_bn_relu_bwd_multi_absmax(dtype, nseg, segs, x, x_c_off, x_c_stride, m, c, mean, invstd, dx, ws, ws_bytes,
+                                     nullptr, stream);
+}
+
+JR_API int jr_bn_relu_bwd_multi_absmax(int dtype, int nseg, const jr_bn_seg* segs, const void* x, int32_t x_c_off,
+                                       int32_t x_c_stride, int64_t m, int32_t c, const float* mean,
+                                       const float* invstd, void* dx, void* ws, size_t ws_bytes, float* dx_absmax,
+                                       void* stream) {
   BnSegs sg;
   const int rc = bwd_setup(dtype, nseg, segs, x, x_c_off, x_c_stride, m, c, mean, invstd, dx, sg);
   if (rc) return rc;
+  sg.absmax = dx_absmax;
   return bn_bwd_launch(dtype, sg, x, x_c_stride, m, c, mean, invstd, dx, ws, ws_bytes, as_stream(stream));
 }
 
@@ -1270,6 +1302,14 @@ JR_API int jr_bn_relu_bwd_maxpool(int dtype, const jr_pool_desc* d, const uint8_
                                   void* dy, const void* x, int32_t x_c_stride, const float* mean,
                                   const float* invstd, const float* beta, void* dx, float* dbeta, void* ws,
                                   size_t ws_bytes, void* stream) {
+  return jr_bn_relu_bwd_maxpool_absmax(dtype, d, argmax, pooled_dy, dy, x, x_c_stride, mean, invstd, beta, dx, dbeta,
+                                       ws, ws_bytes, nullptr, stream);
+}
+
+JR_API int jr_bn_relu_bwd_maxpool_absmax(int dtype, const jr_pool_desc* d, const uint8_t* argmax,
+                                         const void* pooled_dy, void* dy, const void* x, int32_t x_c_stride,
+                                         const float* mean, const float* invstd, const float* beta, void* dx,
+                                         float* dbeta, void* ws, size_t ws_bytes, float* dx_absmax, void* stream) {
   if (!d || !argmax || !pooled_dy || !dy || !x || !mean || !invstd || !beta || !dx || !dbeta)
     return fail(JR_ERR_INVALID, "bn_relu_bwd_maxpool: null pointer");
   const int32_t c = d->c;
@@ -1309,6 +1349,7 @@ JR_API int jr_bn_relu_bwd_maxpool(int dtype, const jr_pool_desc* d, const uint8_
   sg.dbeta[0] = dbeta;
   sg.c0[0] = 0;
   sg.c0[1] = c;
+  sg.absmax = dx_absmax;
   hipLaunchKernelGGL((k_bn_finalize<1>), dim3((int)ceil_div(c, 4)), dim3(256), 0, s, part, grid, c, m, 0.f, k1, k2,
                      sg);
   rc = check_launch("bn_bwd finalize");

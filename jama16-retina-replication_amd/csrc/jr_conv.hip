@@ -225,6 +225,14 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // JR_F32_X6H operand scales (wave-uniform)
+  float h_sa = 1.f, h_sb = 1.f;
+  if constexpr (H6) {
+    h_sa = __uint_as_float(__builtin_amdgcn_readfirstlane(
+        __float_as_uint(pow2_scale(g.a_max ? absmax64(g.a_max, lane) : g.a_bnd))));
+    h_sb = __uint_as_float(__builtin_amdgcn_readfirstlane(
+        __float_as_uint(pow2_scale(g.b_max ? absmax64(g.b_max, lane) : g.b_bnd))));
+  }
   const int wm0 = (wave / WGN) * WM;
   const int wn0 = (wave % WGN) * WN;
 
@@ -609,9 +617,9 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
         for (int g8 = 0; g8 < G8; ++g8) {
           SplitFrag16 sa[TM], sb[TN];
 #pragma unroll
-          for (int i = 0; i < TM; ++i) sa[i].init(&af[i][8 * g8], g.h_sa);
+          for (int i = 0; i < TM; ++i) sa[i].init(&af[i][8 * g8], h_sa);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) sb[j].init(&bfr[j][8 * g8], g.h_sb);
+          for (int j = 0; j < TN; ++j) sb[j].init(&bfr[j][8 * g8], h_sb);
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -781,12 +789,13 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   }
   JR_ST(stamp.loop();)
   if constexpr (H6) {        // back from the operands' power-of-two scales (exact)
+    const float ia = 1.f / h_sa, ib = 1.f / h_sb;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] *= g.h_unscale;
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = acc[i][j][r] * ia * ib;
   }
 
   if constexpr (SK) {
@@ -832,6 +841,9 @@ struct Plan {
 // Channel padding of the reduction operand: 16 B DMA pieces hold 4 fp32 or
 // 8 bf16 channels.
 static bool bf16_operands(int dtype) { return dtype == JR_BF16 || dtype == JR_F32_X8P; }
+// JR_F32_X6H shares JR_F32_X8's tiles, config ids and plans (its kernels
+// differ only in the split: fp16, six products, scaled operands)
+static bool x8_family(int dtype) { return dtype == JR_F32_X8 || dtype == JR_F32_X6H; }
 static int chan_pad(int c, int dtype) {
   const int q = bf16_operands(dtype) ? 8 : 4;
   return (c + q - 1) / q * q;
@@ -859,19 +871,19 @@ static int wide_count(int dtype) {
 // first stream-K id: JR_F32_X8 [28, 42) = the stream-K grid of x8 tile
 // (id - 28) (k_conv SK); JR_BF16 see above
 static int sk_base(int dtype) {
-  return dtype == JR_F32_X8 ? 2 * kNumCfgs : dtype == JR_BF16 ? wide_base(dtype) + kNumCfgsBf16W : 1 << 20;
+  return x8_family(dtype) ? 2 * kNumCfgs : dtype == JR_BF16 ? wide_base(dtype) + kNumCfgsBf16W : 1 << 20;
 }
 static int cfg_count(int dtype) {
   return dtype == JR_BF16 ? sk_base(dtype) + kNumCfgsBf16 + kNumCfgsBf16W
          : dtype == JR_F32_X8P ? wide_base(dtype) + kNumCfgsX8PW
-         : dtype == JR_F32_X8 ? 3 * kNumCfgs
+         : x8_family(dtype) ? 3 * kNumCfgs
          : std_count(dtype);
 }
 static bool is_halo(int dtype, int tile) {
   return dtype == JR_BF16 && tile >= kNumCfgsBf16 && tile < kNumCfgsBf16 + kNumHaloBf16;
 }
 static bool is_wide(int dtype, int tile) { return tile >= wide_base(dtype) && tile < wide_base(dtype) + wide_count(dtype); }
-static bool is_x8_f32(int dtype, int tile) { return dtype == JR_F32_X8 && tile >= kNumCfgs && tile < 2 * kNumCfgs; }
+static bool is_x8_f32(int dtype, int tile) { return x8_family(dtype) && tile >= kNumCfgs && tile < 2 * kNumCfgs; }
 static bool is_sk(int dtype, int tile) { return tile >= sk_base(dtype) && tile < cfg_count(dtype); }
 // the (non-stream-K) id whose tile a stream-K id runs
 static int sk_tile(int dtype, int tile) {
@@ -939,7 +951,7 @@ static int split_target(int dtype, int op, long long K) {
   }();
   if (op != OP_WGRAD) return 640;
   if (wg > 0) return wg;
-  if (dtype == JR_F32_X8 || dtype == JR_F32_X8P) return kmax > 0 && K > kmax ? 640 : 384;
+  if (x8_family(dtype) || dtype == JR_F32_X8P) return kmax > 0 && K > kmax ? 640 : 384;
   return 640;
 }
 
@@ -1116,18 +1128,9 @@ static void launch_op(int cfg, const ConvArgs& a, dim3 grid, hipStream_t s) {
   }
 }
 
-// H6 probe switch (jr_debug_x8_f16): JR_F32_X8 launches of the non-stream-K
-// tiles run the fp16 six-product kernel with these operand scales
-static struct { int on; float sa, sb; } g_x6h = {0, 1.f, 1.f};
-JR_API int jr_debug_x8_f16(int on, float sa, float sb) {
-  g_x6h.on = on;
-  g_x6h.sa = sa;
-  g_x6h.sb = sb;
-  return JR_OK;
-}
 
 static int validate(const jr_conv_desc* d, int op, int dtype) {
-  if (dtype != JR_F32 && dtype != JR_BF16 && dtype != JR_F32_X8 && dtype != JR_F32_X8P)
+  if (dtype != JR_F32 && dtype != JR_BF16 && dtype != JR_F32_X8 && dtype != JR_F32_X8P && dtype != JR_F32_X6H)
     return fail(JR_ERR_INVALID, "conv: bad dtype");
   const int q = bf16_operands(dtype) ? 8 : 4;   // channels per 16 B piece
   if (!d) return fail(JR_ERR_INVALID, "conv: null descriptor");
@@ -1166,6 +1169,18 @@ static void fill_common(ConvArgs& a, const jr_conv_desc* d, int dtype) {
   a.kh = d->kh; a.kw = d->kw; a.sh = d->stride_h; a.sw = d->stride_w;
   a.ph = d->pad_h; a.pw = d->pad_w; a.ho = d->ho; a.wo = d->wo;
   a.xo = d->x_c_off; a.xs = d->x_c_stride; a.yo = d->y_c_off; a.ys = d->y_c_stride;
+}
+
+// JR_F32_X6H: the magnitude bounds of the op's A and B operands (FWD x, w;
+// DGRAD dy, w; WGRAD x, dy) from the descriptor
+static void fill_scales(ConvArgs& a, const jr_conv_desc* d, int op, int dtype) {
+  if (dtype != JR_F32_X6H) return;
+  const float* xm = d->x_absmax;  const float xb = d->x_bound;
+  const float* wm = d->w_absmax;  const float wb = d->w_bound;
+  const float* gm = d->dy_absmax; const float gb = d->dy_bound;
+  if (op == OP_FWD) { a.a_max = xm; a.a_bnd = xb; a.b_max = wm; a.b_bnd = wb; }
+  else if (op == OP_DGRAD) { a.a_max = gm; a.a_bnd = gb; a.b_max = wm; a.b_bnd = wb; }
+  else { a.a_max = xm; a.a_bnd = xb; a.b_max = gm; a.b_bnd = gb; }
 }
 
 #ifdef JR_STAMPS
@@ -1320,12 +1335,11 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
       launch_conv_bf16(OP, p.tile, am, a, grid, s, dtype == JR_F32_X8P ? 3 : 1);
   } else if (is_x8_f32(dtype, p.tile)) {
     launch_op<OP>(p.tile - kNumCfgs, a, grid, s);     // the fp32-MFMA kernel of that tile
+  } else if (p.sk && dtype == JR_F32_X6H) {
+    launch_op<OP, 0, true, true, true>(p.tile - 2 * kNumCfgs, a, grid, s);   // stream-K grid, fp16 six products
   } else if (p.sk) {
     launch_op<OP, 0, true, true>(p.tile - 2 * kNumCfgs, a, grid, s);   // the stream-K grid of that x8 tile
-  } else if (dtype == JR_F32_X8 && g_x6h.on) {
-    a.h_sa = g_x6h.sa;
-    a.h_sb = g_x6h.sb;
-    a.h_unscale = 1.f / (g_x6h.sa * g_x6h.sb);
+  } else if (dtype == JR_F32_X6H) {
     launch_op<OP, 0, true, false, true>(p.tile, a, grid, s);
   } else if (dtype == JR_F32_X8) {
     launch_op<OP, 0, true>(p.tile, a, grid, s);
@@ -1425,6 +1439,7 @@ static int run_conv(const jr_conv_desc* d, int op, int dtype, const void* A, con
     return fail(JR_ERR_INVALID, "conv: tensors must be 16-byte aligned");
   ConvArgs a{};
   fill_common(a, d, dtype);
+  fill_scales(a, d, op, dtype);
   a.A = static_cast<const float*>(A);   // bf16 kernels reinterpret
   a.B = static_cast<const float*>(B);
   a.accumulate = accumulate;
@@ -1728,6 +1743,7 @@ JR_API int jr_conv2d_bwd_filter_slabs(const jr_conv_desc* d, int dtype, const vo
                                 "(tile configuration changed since jr_conv2d_wgrad_seg); re-bind the segment");
   ConvArgs a{};
   fill_common(a, d, dtype);
+  fill_scales(a, d, OP_WGRAD, dtype);
   a.A = static_cast<const float*>(x);
   a.B = static_cast<const float*>(dy);
   if (dtype == JR_F32_X8P) {
@@ -1860,7 +1876,7 @@ JR_API int jr_conv2d_autotune(const jr_conv_desc* d, int op, int dtype, const vo
 }
 
 JR_API int jr_conv2d_num_configs(int dtype) {
-  return dtype == JR_BF16 || dtype == JR_F32 || dtype == JR_F32_X8 || dtype == JR_F32_X8P ? cfg_count(dtype) : 0;
+  return dtype == JR_BF16 || dtype == JR_F32 || x8_family(dtype) || dtype == JR_F32_X8P ? cfg_count(dtype) : 0;
 }
 
 // Diagnostic: time `reps` launches of one FWD GEMM (no split-K) of tile

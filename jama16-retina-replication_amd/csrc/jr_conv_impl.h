@@ -56,9 +56,31 @@ struct ConvArgs {
   float* sk_part;
   // the library's device error word (jr_device_check)
   unsigned* sk_err;
-  // fp16 six-product probe (jr_debug_x8_f16): operand scales, 1 / (sa sb)
-  float h_sa, h_sb, h_unscale;
+  // JR_F32_X6H: magnitude bounds of the A / B operands for their
+  // power-of-two scales: 64 device floats whose max is max |operand|
+  // (nullptr: the host bound a_bnd / b_bnd; 0 = 2^14, scale 1)
+  const float* a_max;
+  const float* b_max;
+  float a_bnd, b_bnd;
 };
+
+// max of the 64 floats at p (every lane of the wave gets it)
+__device__ __forceinline__ float absmax64(const float* p, int lane) {
+  float v = p[lane];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 2^k with m 2^k in [2^14, 2^15) (m = 0, inf or NaN: 1; k <= 100): the
+// JR_F32_X6H operand scale for a tensor whose largest magnitude is m
+__device__ __forceinline__ float pow2_scale(float m) {
+  const unsigned b = __float_as_uint(m);
+  const int eb = (int)((b >> 23) & 0xffu);
+  if (!(m > 0.f) || eb == 255) return 1.f;
+  const int biased = min(268 - eb, 227);
+  return __uint_as_float((unsigned)biased << 23);
+}
 
 // Moves a grouped GEMM's operand / output pointers to member blockIdx.y
 // (a no-op for ordinary launches, gridDim.y == 1).

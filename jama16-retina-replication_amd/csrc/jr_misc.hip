@@ -373,6 +373,42 @@ JR_API int jr_split_x8p(const float* src, int64_t rows, int32_t c, int32_t src_o
   return check_launch("split_x8p");
 }
 
+// jr_absmax_prep: per segment, the max |src| of [off, off + count) raised
+// into out[seg.out * 64 + blockIdx.x % 64] (atomicMax on the bits of each
+// block's max); a segment with limit > 0 whose max exceeds it counts one
+// failure per such block into the device error word.  grid (blocks, nseg).
+__global__ void __launch_bounds__(256) k_absmax_segs(const float* __restrict__ src, const jr_absmax_seg* __restrict__ segs,
+                                                     float* out, unsigned* err) {
+  const jr_absmax_seg sg = segs[blockIdx.y];
+  float v = 0.f;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.count; i += step)
+    v = fmaxf(v, fabsf(src[sg.off + i]));
+  __shared__ float s_max[4];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float b = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
+    atomicMax(reinterpret_cast<unsigned*>(out) + (int64_t)sg.out * 64 + (blockIdx.x & 63), __float_as_uint(b));
+    if (sg.limit > 0.f && !(b <= sg.limit) && err) atomicAdd(err, 1u);
+  }
+}
+
+JR_API int jr_absmax_prep(const float* src, const jr_absmax_seg* segs, int32_t nseg, float* out,
+                          int64_t zero_floats, void* stream) {
+  if (!src || !segs || !out || nseg <= 0 || nseg > 65535 || zero_floats < 0)
+    return fail(JR_ERR_INVALID, "absmax_prep: bad arguments");
+  hipStream_t s = as_stream(stream);
+  if (zero_floats && hipMemsetAsync(out, 0, (size_t)zero_floats * sizeof(float), s) != hipSuccess)
+    return fail(JR_ERR_HIP, "absmax_prep: memset failed");
+  unsigned* err = device_error_word(s);
+  if (!err) return fail(JR_ERR_HIP, "absmax_prep: no device error word (call jr_init before capturing)");
+  hipLaunchKernelGGL(k_absmax_segs, dim3(64, nseg), dim3(256), 0, s, src, segs, out, err);
+  return check_launch("absmax_prep");
+}
+
 JR_API int jr_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream) {
   if (!src || !dst || n < 0) return fail(JR_ERR_INVALID, "cast: bad arguments");
   if (n == 0) return JR_OK;

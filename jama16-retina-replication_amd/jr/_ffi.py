@@ -21,6 +21,7 @@ JR_F32 = 0
 JR_BF16 = 1
 JR_F32_X8 = 2      # conv entry points only: fp32 tensors, bf16x8-split MFMA products (jr.h)
 JR_F32_X8P = 3     # conv entry points only: the X8 arithmetic on pre-split h/m/l bf16 operand planes (jr.h)
+JR_F32_X6H = 4     # conv entry points only: fp32 tensors, scaled fp16 three-way split, six f16 MFMAs (jr.h)
 JR_CONV_FWD, JR_CONV_BWD_DATA, JR_CONV_BWD_FILTER = 0, 1, 2
 JR_HEAD_SIGMOID, JR_HEAD_SOFTMAX = 0, 1
 
@@ -36,7 +37,10 @@ class JRError(RuntimeError):
 class ConvDesc(Structure):
     _fields_ = [(n, c_int32) for n in (
         "n", "h", "w", "c_in", "c_out", "kh", "kw", "stride_h", "stride_w", "pad_h", "pad_w",
-        "ho", "wo", "x_c_off", "x_c_stride", "y_c_off", "y_c_stride")]
+        "ho", "wo", "x_c_off", "x_c_stride", "y_c_off", "y_c_stride")] + [
+        # JR_F32_X6H operand magnitude bounds (jr.h): absmax words or host bounds
+        ("x_absmax", c_void_p), ("w_absmax", c_void_p), ("dy_absmax", c_void_p),
+        ("x_bound", ctypes.c_float), ("w_bound", ctypes.c_float), ("dy_bound", ctypes.c_float)]
 
 
 class WPrep(Structure):
@@ -44,6 +48,11 @@ class WPrep(Structure):
     _fields_ = [("src_off", c_int64), ("hwio_off", c_int64), ("wt_off", c_int64), ("kh", c_int32),
                 ("kw", c_int32), ("c_in", c_int32), ("c_out", c_int32), ("tile_start", c_int32),
                 ("reserved", c_int32)]
+
+
+class AbsmaxSeg(Structure):
+    """include/jr.h jr_absmax_seg: one parameter block of jr_absmax_prep."""
+    _fields_ = [("off", c_int64), ("count", c_int64), ("out", c_int32), ("limit", c_float)]
 
 
 class BnSeg(Structure):
@@ -150,6 +159,9 @@ _SIGS = {
                                c_size_t, c_void_p]),
     "jr_bn_relu_bwd_multi": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int32,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "jr_bn_relu_bwd_multi_absmax": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int32,
+                                            c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
+    "jr_absmax_prep": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
     "jr_maxpool3x3s2_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p,
                                     c_void_p]),
     "jr_bn_relu_maxpool3x3s2_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -158,6 +170,9 @@ _SIGS = {
     "jr_bn_relu_bwd_maxpool": (c_int, [c_int, POINTER(PoolDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                        c_void_p]),
+    "jr_bn_relu_bwd_maxpool_absmax": (c_int, [c_int, POINTER(PoolDesc), c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_size_t, c_void_p, c_void_p]),
     "jr_bn_relu_maxpool3x3s2_fwd_grouped": (c_int, [POINTER(PoolDesc), c_int, c_int32, c_void_p, c_void_p, c_void_p,
                                                     c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "jr_maxpool3x3s2_bwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p, c_int,
@@ -198,7 +213,6 @@ _SIGS = {
     "jr_event_destroy": (c_int, [c_void_p]),
     "jr_device_check": (c_int, []),
     "jr_debug_poison_sk_counts": (c_int, [c_void_p, ctypes.c_uint32]),
-    "jr_debug_x8_f16": (c_int, [c_int, ctypes.c_float, ctypes.c_float]),
 }
 
 EXPORTED = tuple(_SIGS)

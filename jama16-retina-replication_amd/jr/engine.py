@@ -95,9 +95,10 @@ class Engine:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if conv_math is None:            # fp32 default: x8 (fp32-accurate, on the bf16 matrix cores)
             conv_math = "x8" if dtype == "f32" else "bf16"
-        if (dtype == "f32" and conv_math not in ("f32", "x8", "x8p")) or (dtype == "bf16" and conv_math != "bf16"):
-            raise ValueError("conv_math: 'x8', 'x8p' or 'f32' for dtype f32 (x8 = JR_F32_X8, x8p = JR_F32_X8P "
-                             "on pre-split operand planes, f32 = fp32 MFMA); 'bf16' for dtype bf16")
+        if (dtype == "f32" and conv_math not in ("f32", "x8", "x8p", "x6h")) or (dtype == "bf16" and conv_math != "bf16"):
+            raise ValueError("conv_math: 'x8', 'x8p', 'x6h' or 'f32' for dtype f32 (x8 = JR_F32_X8, x8p = JR_F32_X8P "
+                             "on pre-split operand planes, x6h = JR_F32_X6H scaled fp16 split, f32 = fp32 MFMA); "
+                             "'bf16' for dtype bf16")
         if not torch.cuda.is_available():
             raise RuntimeError("jr.Engine needs a ROCm GPU (libjr has no CPU path)")
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
@@ -112,7 +113,13 @@ class Engine:
         # exact three-way split (jr.h); everything else runs self.dt
         self.conv_math = conv_math
         self.x8p = conv_math == "x8p"
-        self.cdt = {"x8": _ffi.JR_F32_X8, "x8p": _ffi.JR_F32_X8P}.get(conv_math, self.dt)
+        # JR_F32_X6H: every conv operand's power-of-two scale from its largest
+        # magnitude -- filters and data gradients measured on the device
+        # (jr_absmax_prep once per step, the BN backward's fused max), the
+        # activations from the bound |relu(xhat + beta)| <= sqrt(N - 1) +
+        # max |beta| (Samuelson), beta guarded on the device (jr.h)
+        self.x6h = conv_math == "x6h"
+        self.cdt = {"x8": _ffi.JR_F32_X8, "x8p": _ffi.JR_F32_X8P, "x6h": _ffi.JR_F32_X6H}.get(conv_math, self.dt)
         self.train_mode = train
         if optimizer not in ("nesterov", "momentum", "sgd", "adam"):
             raise ValueError(f"unknown optimizer {optimizer}")
@@ -291,7 +298,7 @@ class Engine:
             # sets already overlap on the two lanes): their raw gradients live in
             # two alternating sets of per-layer buffers
             self.bn_batch = (self._bn_batch_groups(B)
-                             if not self.x8p and os.environ.get("JR_BN_BATCH", "0") == "1" else [])
+                             if not self.x8p and not self.x6h and os.environ.get("JR_BN_BATCH", "0") == "1" else [])
             slots = max((len(grp) for grp in self.bn_batch), default=0)
             self.drawb = [[self._t(max(B * grp[k].ho * grp[k].wo * grp[k].cout
                                        for grp in self.bn_batch if k < len(grp)), at) for k in range(slots)]
@@ -318,6 +325,40 @@ class Engine:
         self.ws_stem = (self._t((self.ws_bytes + 15) // 4 + 4)
                         if self.train_mode and getattr(self, "draw_stem2", None) is not None else None)
         self.ws = self.ws_lane[0]
+        if self.x6h:
+            self._alloc_absmax(B)
+
+    def _alloc_absmax(self, B: int) -> None:
+        """JR_F32_X6H magnitude words: 64 floats per conv launch for its
+        filter block (rows 0..U-1) and for its raw-output gradient (rows
+        U..2U-1), and the jr_absmax_prep table (filters, then every BN beta
+        with the activation guard)."""
+        U = len(self.cunits)
+        self.absmax = self._t(64 * 2 * U)
+        self._arow = {u.first.idx: k for k, u in enumerate(self.cunits)}
+        nmax = max(B * u.ho * u.wo for u in self.cunits)
+        # activations are BN + ReLU outputs (or pools of them): |y| <= sqrt(N-1)
+        # + max |beta|; bound = a power of two >= sqrt(N_max) + 1024, beta
+        # guarded at that bound, so |y| <= 2 bound < the 4 bound the scale
+        # keeps representable
+        self.act_bound = float(2 ** int(np.ceil(np.log2(np.sqrt(nmax) + 1024))))
+        segs = [_ffi.AbsmaxSeg(u.koff, u.kh * u.kw * u.cin * u.cout, k, 0.0) for k, u in enumerate(self.cunits)]
+        for u in self.cunits:
+            for m in u.members:
+                off = self.plan.poff[f"batch_normalization_{m.idx + 1}/beta"]
+                segs.append(_ffi.AbsmaxSeg(off, m.cout, 2 * U - 1, self.act_bound))
+        # (the betas' maxima land in the last gradient row, zeroed again by
+        # the same prep and raised by the first BN backward only after it:
+        # harmless, a larger bound; conv2d_1's data gradient is never used)
+        arr = (_ffi.AbsmaxSeg * len(segs))(*segs)
+        self.absmax_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
+        self.absmax_nseg = len(segs)
+
+    def _wmax(self, u: ConvUnit) -> int:
+        return self.absmax.data_ptr() + 4 * 64 * self._arow[u.first.idx]
+
+    def _dmax(self, u: ConvUnit) -> int:
+        return self.absmax.data_ptr() + 4 * 64 * (len(self.cunits) + self._arow[u.first.idx])
 
     def _bn_batch_groups(self, B: int):
         """Conv launches whose BN backwards become due together: every member
@@ -585,8 +626,13 @@ class Engine:
             xs = (u.cin + 7) // 8 * 8
         else:
             xs = self.in_stride if u.x == self.g.input_buf else u.cin
-        return _ffi.ConvDesc(B, u.h, u.w, u.cin, u.cout, u.kh, u.kw, u.stride, u.stride,
-                             u.pad_h, u.pad_w, u.ho, u.wo, 0, xs, 0, u.cout)
+        d = _ffi.ConvDesc(B, u.h, u.w, u.cin, u.cout, u.kh, u.kw, u.stride, u.stride,
+                          u.pad_h, u.pad_w, u.ho, u.wo, 0, xs, 0, u.cout)
+        if self.x6h and hasattr(self, "absmax"):
+            d.x_bound = 1.0 if u.x == self.g.input_buf else self.act_bound    # images: f32(k) * f32(1/255) <= 1
+            d.w_absmax = self._wmax(u)
+            d.dy_absmax = self._dmax(u)
+        return d
 
     def _pool_desc(self, n: PoolNode, B: int) -> _ffi.PoolDesc:
         yb = self.g.bufs[n.y.buf]
@@ -642,6 +688,14 @@ class Engine:
         wkey = ("w16",) if (dt == _ffi.JR_BF16 or x8p) else ("p",)
         if dt == _ffi.JR_BF16 or x8p:
             add(fwd, *self._wprep_call(S[0]), 0, [("p",)], [("w16",)])
+        # x6h: the convs read their filters' magnitude words besides the filters
+        xw = [("wmax",)] if self.x6h else []
+        if self.x6h:
+            # the filters' magnitudes (and the beta guard), and every
+            # gradient row zeroed, before the first conv of the step
+            add(fwd, L.jr_absmax_prep, (self.params.data_ptr(), self.absmax_table.data_ptr(), self.absmax_nseg,
+                                        self.absmax.data_ptr(), self.absmax.numel(), S[0]), "absmax_prep", 0,
+                [("p",)], [("wmax",)] + [("dmax", u.first.idx) for u in self.cunits], nbytes=4 * self.nparam)
         # x8p: conv operands are the split planes of the input buffer, written
         # once (by the lane of its first consumer) when the buffer is complete
         AX = (lambda bid: self.aplanes[bid].data_ptr()) if x8p else A  # noqa: E731
@@ -681,7 +735,7 @@ class Engine:
                     # combines its channels' partials (and stores mean / invstd)
                     add(fwd, L.jr_conv2d_fwd_bn_partials, (ctypes.byref(d), cdt, AX(u.x), self._wf(u), raw, ws, wsb,
                                                            s),
-                        "conv_fwd", ln, ax_reads(u.x) + [wkey], [("r", uid), ("ws", ln)])
+                        "conv_fwd", ln, ax_reads(u.x) + [wkey] + xw, [("r", uid), ("ws", ln)])
                     part = ws.value + lay.ws_offset
                     for m, co in zip(u.members, u.col_off):
                         yb = g.bufs[m.y.buf]
@@ -696,7 +750,7 @@ class Engine:
                 add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), cdt, AX(u.x), self._wf(u), raw, BN_EPS,
                                                     self.mean_unit[uid].data_ptr(),
                                                     self.invstd_unit[uid].data_ptr(), ws, wsb, s),
-                    "conv_fwd", ln, ax_reads(u.x) + [wkey], [("r", uid), ("ws", ln)])
+                    "conv_fwd", ln, ax_reads(u.x) + [wkey] + xw, [("r", uid), ("ws", ln)])
                 if (self.apply_multi and len(u.members) > 1 and u.cout // self._vw <= 256
                         and not any(m.y.buf in fused_bufs for m in u.members)):
                     # every member's BN + ReLU in one launch (jr_bn_relu_apply_multi)
@@ -876,15 +930,17 @@ class Engine:
                         pn, m0 = g.nodes[pool_i], u.first
                         pd = self._pool_desc(pn, B)
                         keep.append(pd)
-                        add(bwd, L.jr_bn_relu_bwd_maxpool, (dt, ctypes.byref(pd), self.argmax[pool_i].data_ptr(),
-                                                            D(pn.y.buf), D(pn.x), raw, u.cout,
-                                                            self.mean_unit[uid].data_ptr(),
-                                                            self.invstd_unit[uid].data_ptr(),
-                                                            self._p(f"batch_normalization_{m0.idx + 1}/beta"), draw,
-                                                            self._gp(f"batch_normalization_{m0.idx + 1}/beta"), ws,
-                                                            wsb, s),
+                        pargs = (dt, ctypes.byref(pd), self.argmax[pool_i].data_ptr(), D(pn.y.buf), D(pn.x), raw,
+                                 u.cout, self.mean_unit[uid].data_ptr(), self.invstd_unit[uid].data_ptr(),
+                                 self._p(f"batch_normalization_{m0.idx + 1}/beta"), draw,
+                                 self._gp(f"batch_normalization_{m0.idx + 1}/beta"), ws, wsb)
+                        pfn = L.jr_bn_relu_bwd_maxpool
+                        if self.x6h:    # also the raw-output gradient's magnitude (dy_absmax of its GEMMs)
+                            pfn, pargs = L.jr_bn_relu_bwd_maxpool_absmax, pargs + (self._dmax(u),)
+                        add(bwd, pfn, pargs + (s,),
                             "bn_relu_bwd", ln, [("d", pn.y.buf, pn.y.c_off), ("am", pool_i), ("r", uid), ("p",)],
-                            d_all(pn.x) + [dkey, ("g", uid), ("ws", ln)], nbytes=4 * M * u.cout * self.esz)
+                            d_all(pn.x) + [dkey, ("g", uid), ("ws", ln)] + ([("dmax", uid)] if self.x6h else []),
+                            nbytes=4 * M * u.cout * self.esz)
                     for grp in ([] if pool_i is not None or uid in batch_draw else self._bn_groups(u)):
                         co0 = grp[0][1]
                         cg = sum(m.cout for m, _ in grp)
@@ -893,12 +949,16 @@ class Engine:
                                        self._p(f"batch_normalization_{m.idx + 1}/beta"),
                                        self._gp(f"batch_normalization_{m.idx + 1}/beta")) for m, _ in grp])
                         keep.append(segs)
-                        add(bwd, L.jr_bn_relu_bwd_multi, (dt, len(grp), ctypes.byref(segs), raw, co0, u.cout, M, cg,
-                                                          self.mean_unit[uid].data_ptr() + 4 * co0,
-                                                          self.invstd_unit[uid].data_ptr() + 4 * co0, draw, ws, wsb,
-                                                          s),
+                        bargs = (dt, len(grp), ctypes.byref(segs), raw, co0, u.cout, M, cg,
+                                 self.mean_unit[uid].data_ptr() + 4 * co0, self.invstd_unit[uid].data_ptr() + 4 * co0,
+                                 draw, ws, wsb)
+                        bfn = L.jr_bn_relu_bwd_multi
+                        if self.x6h:
+                            bfn, bargs = L.jr_bn_relu_bwd_multi_absmax, bargs + (self._dmax(u),)
+                        add(bwd, bfn, bargs + (s,),
                             "bn_relu_bwd", ln, [("d", m.y.buf, m.y.c_off) for m, _ in grp] + [("r", uid), ("p",)],
-                            [dkey, ("g", uid), ("ws", ln)], nbytes=3 * M * cg * self.esz)
+                            [dkey, ("g", uid), ("ws", ln)] + ([("dmax", uid)] if self.x6h else []),
+                            nbytes=3 * M * cg * self.esz)
                     if x8p:             # the raw-output gradient as split planes (dgrad and wgrad operand)
                         drawp = self.drawp_lane[ln].data_ptr()
                         add(bwd, L.jr_split_x8p, (draw, M, u.cout, 0, u.cout, drawp, u.cout, 0, u.cout, M * u.cout, s),
@@ -908,7 +968,7 @@ class Engine:
                         if u.x != g.input_buf:
                             add(bwd, L.jr_conv2d_bwd_data, (ctypes.byref(d), cdt, draw, self._wd(u), D(u.x), acc, ws,
                                                             wsb, s),
-                                "conv_dgrad", ln, [dkey, wkey], d_all(u.x) + [("ws", ln)])
+                                "conv_dgrad", ln, [dkey, wkey] + xw, d_all(u.x) + [("ws", ln)])
                             written.add(u.x)
                     if self.dgrad_first:
                         dgrad()

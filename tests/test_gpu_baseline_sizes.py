@@ -9,7 +9,7 @@ Each fixture also holds the same step computed by the fp32 CPU restatement
 envelope fp32 rounding alone produces on THIS step.
 
 fp32 engines (x8 = the fp32 default, f32 = fp32 MFMA, x8p = pre-split
-operands): logits rel-err <= 1e-3 (north star) and <= 3x the fp32-CPU
+operands, x6h = scaled fp16 split with six products): logits rel-err <= 1e-3 (north star) and <= 3x the fp32-CPU
 envelope (+1e-6); loss within 3x the envelope (+1e-6); per-tensor gradient
 norm and Rademacher-projection errors: median and max over the 190 tensors
 within 3x the fp32-CPU median / max (+1e-6).  At B = 64 every BN population
@@ -96,6 +96,8 @@ CASES = [
     pytest.param("net_res299_b64.npz", "f32", "x8", id="299b64-f32x8"),
     pytest.param("net_res299_b64.npz", "f32", "f32", id="299b64-f32mfma"),
     pytest.param("net_res299_b64.npz", "f32", "x8p", id="299b64-f32x8p"),
+    pytest.param("net_res299_b64.npz", "f32", "x6h", id="299b64-f32x6h"),
+    pytest.param("net_res587_b2.npz", "f32", "x6h", id="587b2-f32x6h"),
     pytest.param("net_res587_b2.npz", "f32", "x8", id="587b2-f32x8"),
     pytest.param("net_res299_b64.npz", "bf16", None, id="299b64-bf16"),
     pytest.param("net_res587_b2.npz", "bf16", None, id="587b2-bf16"),

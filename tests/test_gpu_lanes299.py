@@ -11,14 +11,14 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_two_lanes_bitwise_one_lane_299_b64_pinned(dtype):
+@pytest.mark.parametrize("dtype,math", [("f32", None), ("bf16", None), ("f32", "x6h")])
+def test_two_lanes_bitwise_one_lane_299_b64_pinned(dtype, math):
     from jr import synth
     from jr.engine import Engine
     x, y = synth.fundus_batch(0, 64, 299), synth.labels(0, 64)
     out = {}
     for lanes in (1, 2):
-        e = Engine(64, 299, 299, dtype=dtype, seed=0, lanes=lanes)
+        e = Engine(64, 299, 299, dtype=dtype, seed=0, lanes=lanes, conv_math=math)
         assert e.tiles == "pinned"
         if dtype == "f32":        # the fp32 table's stream-K grids are in play
             sk = sum(1 for f, wg, dg in e.conv_configs().values() for c in [f, wg, *dg]

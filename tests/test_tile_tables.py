@@ -12,9 +12,9 @@ import pytest
 from conftest import PKG
 
 TABLES = os.path.join(PKG, "jr", "tiles_mi355x.json")
-CDT = {"x8": 2, "x8p": 3, "f32": 0, "bf16": 1}
+CDT = {"x8": 2, "x8p": 3, "f32": 0, "bf16": 1, "x6h": 4}
 WANT = {("x8", 64, 299, True), ("bf16", 64, 299, True), ("x8", 32, 299, False), ("bf16", 32, 299, False),
-        ("bf16", 64, 587, True)}
+        ("bf16", 64, 587, True), ("x6h", 64, 299, True)}
 
 
 def _tables():
