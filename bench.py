@@ -65,9 +65,11 @@ def parse():
                     help="ensemble mode: one engine per member instead of the grouped EnsembleEngine")
     ap.add_argument("--res", type=int, default=299)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
-    ap.add_argument("--conv-math", default="x8", choices=["f32", "x8", "x8p", "x6h"],
-                    help="dtype f32 only. x8 (default): fp32 tensors, products from an exact 3-way bf16 split "
-                         "(jr.h JR_F32_X8, fp32-accurate); f32: fp32 MFMA")
+    ap.add_argument("--conv-math", default="x6h", choices=["f32", "x8", "x8p", "x6h"],
+                    help="dtype f32 only. x6h (default): fp32 tensors, products from a power-of-two-scaled 3-way "
+                         "fp16 split, six f16 MFMAs (jr.h JR_F32_X6H; fp32-accurate, 4.5 %% faster than x8, "
+                         "profiles/r06_ab_x6h_*.txt); x8: exact 3-way bf16 split, eight bf16 MFMAs (JR_F32_X8, "
+                         "the library default); f32: fp32 MFMA")
     # eager launches on two lanes only: round 2 measured them 1.3-1.5 % faster
     # than HIP-graph replay (profiles/r02c_graph_ab.txt), and the measured path
     # keeps no graph code (Engine.capture stays an opt-in, separately tested API)
@@ -186,8 +188,8 @@ def pmc_traffic(dtype: str, B: int, res: int, math: str = "x8") -> dict:
     cannot run the profiler itself, so `traffic` is null without that file."""
     if (B, res) != (64, 299):
         return {}
-    tag = {"f32": "f32mfma", "x8p": "f32x8p"}.get(math, "f32") if dtype == "f32" else dtype
-    for rnd in ("r05", "r04", "r03", "r02c", "r02", "r01"):      # the newest committed summary of this workload
+    tag = {"f32": "f32mfma", "x8p": "f32x8p", "x6h": "f32x6h"}.get(math, "f32") if dtype == "f32" else dtype
+    for rnd in ("r06", "r05", "r04", "r03", "r02c", "r02", "r01"):      # the newest committed summary of this workload
         p = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{tag}.json")
         if os.path.exists(p):
             break

@@ -71,9 +71,10 @@ def build_parser():
     p.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
                    help="activation storage and conv arithmetic: f32 (the reference's; default) or bf16 MFMA "
                         "(BASELINE configs 3 and 5; parameters, gradients, momentum and BN statistics stay fp32)")
-    p.add_argument("--conv_math", default="x8", choices=["x8", "x8p", "x6h", "f32"],
-                   help="fp32 convolution arithmetic (--dtype f32): x8 = exact 3-way bf16 split on the matrix cores "
-                        "(fp32-accurate, default), x8p = the same on pre-split operand planes, f32 = fp32 MFMA")
+    p.add_argument("--conv_math", default="x6h", choices=["x8", "x8p", "x6h", "f32"],
+                   help="fp32 convolution arithmetic (--dtype f32): x6h = power-of-two-scaled 3-way fp16 split, six "
+                        "products on the matrix cores (fp32-accurate, default), x8 = exact 3-way bf16 split, eight "
+                        "products, x8p = x8 on pre-split operand planes, f32 = fp32 MFMA")
     p.add_argument("--replica_dump_dir", default=None,
                    help="(data parallel check) every rank writes its parameters after each epoch as "
                         "<dir>/params_e<epoch>_r<rank>.npy (Keras layout, fp32)")

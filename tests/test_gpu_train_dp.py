@@ -43,7 +43,7 @@ def _one_process_epoch0(train_dir, dtype, seed, shuffle_seed):
     import lib.dataset
     from jr.engine import Engine
     eng = Engine(B, RES, RES, device=0, optimizer="nesterov", lr=3e-3, momentum=0.9, seed=seed, dtype=dtype,
-                 conv_math="x8" if dtype == "f32" else "bf16", tiles="pinned")
+                 conv_math="x6h" if dtype == "f32" else "bf16", tiles="pinned")   # train.py's defaults
     ds = lib.dataset.initialize_dataset(train_dir, B, num_workers=8, prefetch_buffer_size=2 * B,
                                         shuffle_buffer_size=2048, image_data_format="channels_last",
                                         num_channels=3, image_dim=[RES, RES], seed=shuffle_seed,
