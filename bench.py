@@ -420,7 +420,7 @@ def ensemble_bench(args) -> dict:
         roof = None
         if rank == 0 and not args.per_member and not args.no_roofline:
             flops, tconv, nconv = grouped_conv_roofline(engines)
-            peak = PEAK_TFLOPS[math if math in ("x8", "x8p") else args.dtype]
+            peak = PEAK_TFLOPS[math if math in ("x8", "x8p", "x6h") else args.dtype]
             ach = flops / tconv / 1e12
             roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": None,
@@ -572,7 +572,7 @@ def main():
         if not args.no_roofline:
             flops, tconv, nconv = conv_roofline(eng)
             ach = flops / tconv / 1e12
-            peak = PEAK_TFLOPS[math if math in ("x8", "x8p") else args.dtype]
+            peak = PEAK_TFLOPS[math if math in ("x8", "x8p", "x6h") else args.dtype]
             roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(ach / peak, 4), "traffic": None,
                     "kernel": f"conv implicit-GEMM {'fwd+dgrad+wgrad' if train else 'fwd'} ({nconv} calls/step)",
