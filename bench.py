@@ -314,10 +314,12 @@ def max_over_ranks(dist, v: float) -> float:
 def grouped_conv_roofline(ens, steps: int = 3):
     """The conv roofline of the grouped ensemble forward (BASELINE config 4):
     HIP events (on the stream each call is enqueued on) bracket every grouped
-    conv + statistics launch, each run alone (the device synchronised before
-    and after it: with two lanes a neighbour launch would share the CUs and
-    inflate its time); algorithmic FLOPs = members x batch x 2 x MACs per
-    image."""
+    conv + statistics launch, each run alone; algorithmic FLOPs = members x
+    batch x 2 x MACs per image.  Every call of the pass, conv or not, runs
+    with the device synchronised before and after it: the lanes' producer
+    waits are not replayed here, so a fully serial pass is what keeps a BN
+    apply or pool on one lane from racing its producer on the other (ADVICE
+    r05), and a neighbour launch from sharing the CUs with a timed conv."""
     from jr import _ffi
     calls, _ = ens._build_calls(ens.batch)
     flops = sum(2 * n.macs_per_image() for n in ens.g.convs) * ens.batch * ens.members
@@ -325,16 +327,16 @@ def grouped_conv_roofline(ens, steps: int = 3):
     for _ in range(steps):
         for c in calls:
             st = ens.lane_streams[c.lane]
+            torch.cuda.synchronize()
             if c.name == "conv_fwd":
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                torch.cuda.synchronize()
                 e0.record(st)
                 rc = c.fn(*c.args)
                 e1.record(st)
-                torch.cuda.synchronize()
                 pairs.append((e0, e1))
             else:
                 rc = c.fn(*c.args)
+            torch.cuda.synchronize()
             if rc:
                 raise _ffi.JRError(c.name, rc, _ffi.last_error())
     ens.synchronize()

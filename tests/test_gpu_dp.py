@@ -34,14 +34,14 @@ def _shard(step, rank, b=B, res=RES):
     return synth.fundus_batch(k, b, res), synth.labels(k, b, p=0.5)
 
 
-def _rank(rank, port, outdir, dtype="f32", payload="f32", b=B, res=RES, steps=STEPS):
+def _rank(rank, port, outdir, dtype="f32", payload="f32", b=B, res=RES, steps=STEPS, math=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     from jr.dist import BucketAllReduce
     from jr.engine import Engine
-    eng = Engine(b, res, res, seed=3, autotune=False, dtype=dtype)
+    eng = Engine(b, res, res, seed=3, autotune=False, dtype=dtype, conv_math=math)
     ar = BucketAllReduce(eng, WORLD, bucket_bytes=8 << 20, payload=payload)
     losses, fences = [], []
     for step in range(steps):
@@ -62,12 +62,13 @@ def _rank(rank, port, outdir, dtype="f32", payload="f32", b=B, res=RES, steps=ST
 # (dtype, payload, batch, resolution, steps): the 107^2 B=4 cases on the
 # planner's tiles, and the bench workload itself -- 299^2 B=64, two lanes, the
 # pinned MI355X tile tables (stream-K grids included) -- fp32 (x8) and bf16
-CASES = [("f32", "f32", B, RES, STEPS), ("bf16", "f32", B, RES, STEPS), ("bf16", "bf16", B, RES, STEPS),
-         ("f32", "f32", 64, 299, 2), ("bf16", "f32", 64, 299, 2)]
+CASES = [("f32", "f32", B, RES, STEPS, None), ("bf16", "f32", B, RES, STEPS, None),
+         ("bf16", "bf16", B, RES, STEPS, None), ("f32", "f32", 64, 299, 2, None), ("bf16", "f32", 64, 299, 2, None),
+         ("f32", "f32", 64, 299, 2, "x6h")]        # (the bench default: JR_F32_X6H convolutions)
 
 
-@pytest.mark.parametrize("dtype,payload,b,res,steps", CASES)
-def test_two_ranks_equal_one_process_averaging_shards(dtype, payload, b, res, steps):
+@pytest.mark.parametrize("dtype,payload,b,res,steps,math", CASES)
+def test_two_ranks_equal_one_process_averaging_shards(dtype, payload, b, res, steps, math):
     """fp32 and bf16 engines (configs 2 and 3), fp32 or bf16 gradient payload.
     The one-process reference sums the two shards' gradients exactly as the
     two-rank all-reduce does: fp32 a + b, or (bf16 payload) each shard's
@@ -80,7 +81,7 @@ def test_two_ranks_equal_one_process_averaging_shards(dtype, payload, b, res, st
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.get_context("spawn")
-        ps = [ctx.Process(target=_rank, args=(r, port, d, dtype, payload, b, res, steps)) for r in range(WORLD)]
+        ps = [ctx.Process(target=_rank, args=(r, port, d, dtype, payload, b, res, steps, math)) for r in range(WORLD)]
         for p in ps:
             p.start()
         for p in ps:
@@ -93,7 +94,7 @@ def test_two_ranks_equal_one_process_averaging_shards(dtype, payload, b, res, st
     for nb, fences, nl, pinned in meta:
         assert 1 <= fences <= nb and nl == 2
         assert pinned == int(res == 299)            # the bench workload runs its committed tile table
-    ref = Engine(b, res, res, seed=3, autotune=False, dtype=dtype)
+    ref = Engine(b, res, res, seed=3, autotune=False, dtype=dtype, conv_math=math)
     ref_losses = [[], []]
     for step in range(steps):
         gsum = None
@@ -162,7 +163,7 @@ def test_jr_comm_rccl_world1(payload, tmp_path):
     comm.close()
 
 
-def _world1_rccl(outdir, dtype):
+def _world1_rccl(outdir, dtype, math=None):
     """Child: a world-1 RCCL group (torch.distributed backend nccl) and the
     bench workload's DP step (bench.py --dp on) next to the plain step."""
     import socket as _s
@@ -175,8 +176,8 @@ def _world1_rccl(outdir, dtype):
     dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
     from jr.dist import BucketAllReduce
     from jr.engine import Engine
-    a = Engine(64, 299, 299, seed=3, dtype=dtype)
-    b = Engine(64, 299, 299, seed=3, dtype=dtype)
+    a = Engine(64, 299, 299, seed=3, dtype=dtype, conv_math=math)
+    b = Engine(64, 299, 299, seed=3, dtype=dtype, conv_math=math)
     ar = BucketAllReduce(b, 1)
     for step in range(2):
         for e in (a, b):
@@ -190,8 +191,8 @@ def _world1_rccl(outdir, dtype):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_world1_rccl_dp_step_equals_plain_step(dtype):
+@pytest.mark.parametrize("dtype,math", [("f32", None), ("bf16", None), ("f32", "x6h")])
+def test_world1_rccl_dp_step_equals_plain_step(dtype, math):
     """The DP machinery at the bench workload (299^2 B=64, two lanes, pinned
     tiles) over a real RCCL group of one rank: buckets issued from the feed
     stream during the backward, lane 0 waiting for them only before the
@@ -199,7 +200,7 @@ def test_world1_rccl_dp_step_equals_plain_step(dtype):
     bucket."""
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:
-        p = mp.get_context("spawn").Process(target=_world1_rccl, args=(d, dtype))
+        p = mp.get_context("spawn").Process(target=_world1_rccl, args=(d, dtype, math))
         p.start()
         p.join(600)
         assert p.exitcode == 0, p.exitcode
