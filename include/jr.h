@@ -167,8 +167,9 @@ int jr_conv2d_fwd_bn_stats(const jr_conv_desc* d, int dtype, const void* x, cons
  * member i reading x + i*x_member_stride and w + i*w_member_stride and
  * writing y + i*y_member_stride, mean / invstd + i*stats_member_stride
  * (strides in elements of each tensor; w = the filter operand of that dtype:
- * fp32 HWIO, or the bf16 W^T copy for JR_BF16).  dtype JR_F32, JR_BF16 or
- * JR_F32_X8.  Each member's plan (tile, split-K) is the per-member plan, so
+ * fp32 HWIO, or the bf16 W^T copy for JR_BF16).  dtype JR_F32, JR_BF16,
+ * JR_F32_X8 or JR_F32_X6H (member i's magnitude words at x_absmax / w_absmax
+ * + 64 i floats).  Each member's plan (tile, split-K) is the per-member plan, so
  * its y, mean and invstd are bitwise those of jr_conv2d_fwd_bn_stats on its
  * own tensors.  Workspace: jr_conv2d_workspace_size_grouped. */
 size_t jr_conv2d_workspace_size_grouped(const jr_conv_desc* d, int dtype, int members);

@@ -1821,8 +1821,8 @@ JR_API int jr_conv2d_fwd_bn_stats_grouped(const jr_conv_desc* d, int dtype, int 
                                           int64_t stats_member_stride, void* ws, size_t ws_bytes, void* stream) {
   int rc = validate(d, OP_FWD, dtype);
   if (rc) return rc;
-  if (dtype != JR_F32 && dtype != JR_BF16 && dtype != JR_F32_X8)
-    return fail(JR_ERR_UNSUPPORTED, "conv grouped: dtype must be JR_F32, JR_BF16 or JR_F32_X8");
+  if (dtype != JR_F32 && dtype != JR_BF16 && dtype != JR_F32_X8 && dtype != JR_F32_X6H)
+    return fail(JR_ERR_UNSUPPORTED, "conv grouped: dtype must be JR_F32, JR_BF16, JR_F32_X8 or JR_F32_X6H");
   if (members < 1 || members > 65535) return fail(JR_ERR_INVALID, "conv grouped: members must be 1..65535");
   if (!x || !w || !y || !mean || !invstd) return fail(JR_ERR_INVALID, "conv grouped: null pointer");
   const long long esz = dtype == JR_BF16 ? 2 : 4;
@@ -1838,6 +1838,7 @@ JR_API int jr_conv2d_fwd_bn_stats_grouped(const jr_conv_desc* d, int dtype, int 
   }
   ConvArgs a{};
   fill_common(a, d, dtype);
+  fill_scales(a, d, OP_FWD, dtype);
   a.A = static_cast<const float*>(x);
   a.B = static_cast<const float*>(w);
   a.accumulate = 0;

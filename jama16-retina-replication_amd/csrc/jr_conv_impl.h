@@ -91,6 +91,9 @@ __device__ __forceinline__ void member_offsets(ConvArgs& g) {
     g.B = reinterpret_cast<const float*>(reinterpret_cast<const char*>(g.B) + m * g.b_mb);
     g.C = reinterpret_cast<float*>(reinterpret_cast<char*>(g.C) + m * g.c_mb);
     if (g.stats) g.stats = reinterpret_cast<float*>(reinterpret_cast<char*>(g.stats) + m * g.s_mb);
+    // JR_F32_X6H grouped: each member's 64 magnitude words follow the previous member's
+    if (g.a_max) g.a_max += 64 * m;
+    if (g.b_max) g.b_max += 64 * m;
     if (g.sk_flags) {
       g.sk_flags = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(g.sk_flags) + m * g.sk_fmb);
       g.sk_part = reinterpret_cast<float*>(reinterpret_cast<char*>(g.sk_part) + m * g.sk_mb);

@@ -61,7 +61,7 @@ def build_parser():
     p.add_argument("-op", "--operating_threshold", default=0.5, help="operating threshold")
     p.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
                    help="activation storage and conv arithmetic: f32 (the reference's; default) or bf16 MFMA")
-    p.add_argument("--conv_math", default="x8", choices=["x8", "x8p", "f32"],
+    p.add_argument("--conv_math", default="x8", choices=["x8", "x8p", "x6h", "f32"],
                    help="fp32 convolution arithmetic: x8 = exact 3-way bf16 split on the matrix cores (fp32-accurate, "
                         "default), x8p = the same on pre-split operand planes, f32 = fp32 MFMA")
     p.add_argument("--per_member", action="store_true",

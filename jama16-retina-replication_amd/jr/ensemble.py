@@ -47,8 +47,8 @@ class EnsembleEngine:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
         if conv_math is None:
             conv_math = "x8" if dtype == "f32" else "bf16"
-        if (dtype == "f32" and conv_math not in ("x8", "f32")) or (dtype == "bf16" and conv_math != "bf16"):
-            raise ValueError("grouped conv math: 'x8' or 'f32' for dtype f32, 'bf16' for dtype bf16")
+        if (dtype == "f32" and conv_math not in ("x8", "x6h", "f32")) or (dtype == "bf16" and conv_math != "bf16"):
+            raise ValueError("grouped conv math: 'x8', 'x6h' or 'f32' for dtype f32, 'bf16' for dtype bf16")
         if not torch.cuda.is_available():
             raise RuntimeError("jr.EnsembleEngine needs a ROCm GPU (libjr has no CPU path)")
         if not params:
@@ -69,7 +69,8 @@ class EnsembleEngine:
         self.batch = int(batch)
         self.dtype, self.dt = dtype, DTYPES[dtype]
         self.conv_math = conv_math
-        self.cdt = _ffi.JR_F32_X8 if conv_math == "x8" else self.dt
+        self.cdt = {"x8": _ffi.JR_F32_X8, "x6h": _ffi.JR_F32_X6H}.get(conv_math, self.dt)
+        self.x6h = conv_math == "x6h"
         self.esz = 2 if self.dt == _ffi.JR_BF16 else 4
         self.head_mode = _ffi.JR_HEAD_SIGMOID if head == "sigmoid" else _ffi.JR_HEAD_SOFTMAX
         self.stream = torch.cuda.Stream(device=self.device)
@@ -146,6 +147,23 @@ class EnsembleEngine:
             self.wprep_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
             self.wprep_layers, self.wprep_tiles = len(layers), M * tiles
             self.w_t = self._t(M * self.wt_ms, torch.bfloat16)
+        if self.x6h:
+            # JR_F32_X6H magnitude words: 64 floats per (launch, member), the
+            # members of a launch contiguous (the grouped conv's convention);
+            # the filters never change in inference: measured at load_params
+            U = len(self.cunits)
+            self.absmax = self._t(64 * (U * M + 1))
+            self._arow = {u.first.idx: k for k, u in enumerate(self.cunits)}
+            nmax = max(B * u.ho * u.wo for u in self.cunits)
+            self.act_bound = float(2 ** int(np.ceil(np.log2(np.sqrt(nmax) + 1024))))   # as jr.Engine
+            segs = [_ffi.AbsmaxSeg(m * self.nparam + u.koff, u.kh * u.kw * u.cin * u.cout, k * M + m, 0.0)
+                    for k, u in enumerate(self.cunits) for m in range(M)]
+            segs += [_ffi.AbsmaxSeg(m * self.nparam + self.plan.poff[f"batch_normalization_{n.idx + 1}/beta"],
+                                    n.cout, U * M, self.act_bound)
+                     for m in range(M) for u in self.cunits for n in u.members]
+            arr = (_ffi.AbsmaxSeg * len(segs))(*segs)
+            self.absmax_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
+            self.absmax_nseg = len(segs)
         ws = 0
         for u in self.cunits:
             d = self._conv_desc(u, B)
@@ -167,13 +185,23 @@ class EnsembleEngine:
                 _ffi.check("wprep", self.lib.jr_conv_weights_bf16_multi(
                     self.wprep_table.data_ptr(), self.wprep_layers, self.wprep_tiles, self.params.data_ptr(), None,
                     self.w_t.data_ptr(), self._s))
+        if self.x6h:
+            _ffi.check("absmax_prep", self.lib.jr_absmax_prep(
+                self.params.data_ptr(), self.absmax_table.data_ptr(), self.absmax_nseg, self.absmax.data_ptr(),
+                self.absmax.numel(), self._s))
         self.stream.synchronize()
+        if self.x6h:
+            _ffi.device_check()       # the beta guard of the activation bound (jr.h jr_absmax_prep)
 
     # ------------------------------------------------------------ descriptors
     def _conv_desc(self, u, B: int) -> _ffi.ConvDesc:
         xs = self.in_stride if u.x == self.g.input_buf else u.cin
-        return _ffi.ConvDesc(B, u.h, u.w, u.cin, u.cout, u.kh, u.kw, u.stride, u.stride,
-                             u.pad_h, u.pad_w, u.ho, u.wo, 0, xs, 0, u.cout)
+        d = _ffi.ConvDesc(B, u.h, u.w, u.cin, u.cout, u.kh, u.kw, u.stride, u.stride,
+                          u.pad_h, u.pad_w, u.ho, u.wo, 0, xs, 0, u.cout)
+        if getattr(self, "x6h", False) and hasattr(self, "absmax"):
+            d.x_bound = 1.0 if u.x == self.g.input_buf else self.act_bound
+            d.w_absmax = self.absmax.data_ptr() + 4 * 64 * self._arow[u.first.idx] * self.members
+        return d
 
     def _apply_configs(self, cfgs: dict) -> None:
         """The per-member forward tile of every launch (the eval table's)."""

@@ -64,6 +64,12 @@ def _conv_case(ffi, L, dt, case, members, cfg=None, seed=3):
         W = torch.randn(members * wm, device="cuda", generator=g) * 0.1
     ym = n * ho * wo * cout
     _KEEP.extend([X, W])
+    if dt == ffi.JR_F32_X6H:    # magnitude words: member m's 64 at +64 m (jr.h grouped convention)
+        words = zeros(64 * members)
+        for m in range(members):
+            words[64 * m + 3] = W[m * wm:(m + 1) * wm].abs().max()
+        d.w_absmax = words.data_ptr()
+        d.x_bound = float(X.abs().max())
     if cfg is not None:
         ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, dt, 0, cfg))
     try:
@@ -80,6 +86,8 @@ def _conv_case(ffi, L, dt, case, members, cfg=None, seed=3):
         esz = 2 if dt == ffi.JR_BF16 else 4
         for m in range(members):
             Y, S = zeros(ym, at), zeros(2 * cout)
+            if dt == ffi.JR_F32_X6H:
+                d.w_absmax = words.data_ptr() + 4 * 64 * m
             ffi.check("single", L.jr_conv2d_fwd_bn_stats(
                 ctypes.byref(d), dt, X.data_ptr() + esz * m * xm, W.data_ptr() + esz * m * wm, Y.data_ptr(), 1e-3,
                 S.data_ptr(), S.data_ptr() + 4 * cout, w1.data_ptr(), ws1, None))
@@ -90,18 +98,20 @@ def _conv_case(ffi, L, dt, case, members, cfg=None, seed=3):
     finally:
         if cfg is not None:
             ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, dt, 0, -1))
+        if dt == ffi.JR_F32_X6H:
+            d.w_absmax = words.data_ptr()
 
 
 CASES = [(4, 17, 17, 192, 192, 1, 7, 1, "same"), (4, 8, 8, 448, 384, 3, 3, 1, "same"),
          (4, 35, 35, 288, 64, 1, 1, 1, "same"), (3, 37, 37, 3, 32, 3, 3, 2, "valid")]
 
 
-@pytest.mark.parametrize("dt", ["f32", "x8", "bf16"])
+@pytest.mark.parametrize("dt", ["f32", "x8", "x6h", "bf16"])
 @pytest.mark.parametrize("case", CASES)
 def test_grouped_conv_equals_members(dt, case):
     ffi = _lib()
     L = ffi.load()
-    code = {"f32": ffi.JR_F32, "x8": ffi.JR_F32_X8, "bf16": ffi.JR_BF16}[dt]
+    code = {"f32": ffi.JR_F32, "x8": ffi.JR_F32_X8, "x6h": ffi.JR_F32_X6H, "bf16": ffi.JR_BF16}[dt]
     _conv_case(ffi, L, code, case, 3)
     for sp in (1, 4):                    # forced split-K: slab / partial member regions
         _conv_case(ffi, L, code, case, 3, cfg=0 | (sp << 8))
@@ -117,9 +127,9 @@ def test_grouped_conv_two_stage_statistics():
         _conv_case(ffi, L, code, (16, 299, 299, 3, 32, 3, 3, 2, "valid"), 2, cfg=tile | (1 << 8))
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("dtype,math", [("f32", None), ("bf16", None), ("f32", "x6h")])
 @pytest.mark.parametrize("res,B,M", [(107, 8, 3), (299, 32, 2)])
-def test_ensemble_engine_equals_engines(dtype, res, B, M):
+def test_ensemble_engine_equals_engines(dtype, math, res, B, M):
     from jr import synth
     from jr.engine import Engine
     from jr.ensemble import EnsembleEngine
@@ -127,7 +137,7 @@ def test_ensemble_engine_equals_engines(dtype, res, B, M):
     from jr.init import init_params
     g = build_inception_v3(res, res)
     params = [init_params(g, 40 + m) for m in range(M)]
-    ens = EnsembleEngine(params, B, res, res, dtype=dtype)
+    ens = EnsembleEngine(params, B, res, res, dtype=dtype, conv_math=math)
     for n in (B, 5):                      # full and partial last batch
         x, y = synth.fundus_batch(100, n, res), synth.labels(100, n, p=0.3)
         ens.set_batch(x, y)
@@ -135,12 +145,12 @@ def test_ensemble_engine_equals_engines(dtype, res, B, M):
         got = ens.predictions(n)
         assert got.shape == (M, n, 1)
         for m in range(M):
-            e = Engine(B, res, res, dtype=dtype, train=False, seed=0)
+            e = Engine(B, res, res, dtype=dtype, train=False, seed=0, conv_math=math)
             e.load_params(params[m])
             e.set_batch(x, y)
             e.forward(n)
             want = e.predictions(n)
-            assert np.array_equal(got[m], want), (dtype, res, n, m, np.abs(got[m] - want).max())
+            assert np.array_equal(got[m], want), (dtype, math, res, n, m, np.abs(got[m] - want).max())
             del e
         assert len({got[m].tobytes() for m in range(M)}) == M     # the members differ
 

@@ -70,15 +70,16 @@ def test_inputs_match_the_fixture(evalset):
 
 
 @pytest.mark.parametrize("grouped", [True, False], ids=["grouped", "per_member"])
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_config4_ensemble_vs_fp64(evalset, dtype, grouped):
+@pytest.mark.parametrize("dtype,math", [("f32", "x8"), ("f32", "x6h"), ("bf16", None)])
+def test_config4_ensemble_vs_fp64(evalset, dtype, math, grouped):
     """grouped=True is evaluate.py's default path (one jr.ensemble.
     EnsembleEngine for every member); per_member is
     --per_member (one jr.Engine each)."""
     import evaluate
     from jr import checkpoint
     data, paths, _ = evalset
-    engines = evaluate.make_engines(paths, checkpoint.read_meta(paths[0]), B, dtype=dtype, grouped=grouped)
+    engines = evaluate.make_engines(paths, checkpoint.read_meta(paths[0]), B, dtype=dtype, grouped=grouped,
+                                    conv_math=math or "x8")
     tiles = [engines.tiles] if grouped else [e.tiles for e in engines]
     assert all(t == "pinned" for t in tiles), tiles
     preds, labels, ids = evaluate.predict_all(engines, data, B)
@@ -89,7 +90,7 @@ def test_config4_ensemble_vs_fp64(evalset, dtype, grouped):
     err = np.abs(got - want).max()
     ens = np.mean(np.array(preds), axis=0)                    # evaluate.py:214-217 (float32)
     auc, brier, conf = _metrics(labels, ens)
-    print(f"config 4 {dtype}: max |pred - fp64| {err:.2e}, AUC {auc:.6f} vs {float(G['auc']):.6f}, "
+    print(f"config 4 {dtype} {math}: max |pred - fp64| {err:.2e}, AUC {auc:.6f} vs {float(G['auc']):.6f}, "
           f"Brier {brier:.6f} vs {float(G['brier']):.6f}")
     if dtype == "f32":
         assert err < 1e-4, err
