@@ -873,26 +873,18 @@ static int wide_count(int dtype) {
 static int sk_base(int dtype) {
   return x8_family(dtype) ? 2 * kNumCfgs : dtype == JR_BF16 ? wide_base(dtype) + kNumCfgsBf16W : 1 << 20;
 }
-// JR_F32_X6H appends its halo-tiled forward configs (kHaloF32) after the
-// x8 id space: ids [42, 42 + kNumHaloF32)
 static int cfg_count(int dtype) {
   return dtype == JR_BF16 ? sk_base(dtype) + kNumCfgsBf16 + kNumCfgsBf16W
          : dtype == JR_F32_X8P ? wide_base(dtype) + kNumCfgsX8PW
-         : dtype == JR_F32_X6H ? 3 * kNumCfgs + kNumHaloF32
-         : dtype == JR_F32_X8 ? 3 * kNumCfgs
+         : x8_family(dtype) ? 3 * kNumCfgs
          : std_count(dtype);
 }
-static int sk_end(int dtype) { return x8_family(dtype) ? 3 * kNumCfgs : cfg_count(dtype); }
 static bool is_halo(int dtype, int tile) {
-  if (dtype == JR_F32_X6H) return tile >= 3 * kNumCfgs && tile < 3 * kNumCfgs + kNumHaloF32;
   return dtype == JR_BF16 && tile >= kNumCfgsBf16 && tile < kNumCfgsBf16 + kNumHaloBf16;
-}
-static const HaloCfg& halo_cfg(int dtype, int tile) {
-  return dtype == JR_F32_X6H ? kHaloF32[tile - 3 * kNumCfgs] : kHaloBf16[tile - kNumCfgsBf16];
 }
 static bool is_wide(int dtype, int tile) { return tile >= wide_base(dtype) && tile < wide_base(dtype) + wide_count(dtype); }
 static bool is_x8_f32(int dtype, int tile) { return x8_family(dtype) && tile >= kNumCfgs && tile < 2 * kNumCfgs; }
-static bool is_sk(int dtype, int tile) { return tile >= sk_base(dtype) && tile < sk_end(dtype); }
+static bool is_sk(int dtype, int tile) { return tile >= sk_base(dtype) && tile < cfg_count(dtype); }
 // the (non-stream-K) id whose tile a stream-K id runs
 static int sk_tile(int dtype, int tile) {
   const int k = tile - sk_base(dtype);
@@ -900,7 +892,7 @@ static int sk_tile(int dtype, int tile) {
 }
 static const TileCfg& tile_cfg(int dtype, int tile) {
   if (is_sk(dtype, tile)) tile = sk_tile(dtype, tile);
-  if (is_halo(dtype, tile)) return halo_cfg(dtype, tile).t;
+  if (is_halo(dtype, tile)) return kHaloBf16[tile - kNumCfgsBf16].t;
   if (is_wide(dtype, tile)) return (dtype == JR_BF16 ? kCfgsBf16W : kCfgsX8PW)[tile - wide_base(dtype)];
   if (is_x8_f32(dtype, tile)) return kCfgs[tile - kNumCfgs];
   return (dtype == JR_BF16 ? kCfgsBf16 : dtype == JR_F32_X8P ? kCfgsX8P : kCfgs)[tile];
@@ -909,10 +901,9 @@ static const TileCfg& tile_cfg(int dtype, int tile) {
 static int halo_rows(const jr_conv_desc* d, int bm) { return (bm + d->wo - 2) / d->wo + 1 + d->kh - 1; }
 static bool halo_ok(const jr_conv_desc* d, int op, int dtype, int tile) {
   if (!is_halo(dtype, tile) || op != OP_FWD) return false;
-  const HaloCfg& h = halo_cfg(dtype, tile);
-  const int chunk = dtype == JR_F32_X6H ? 16 : 32;   // channels per slot
+  const HaloCfg& h = kHaloBf16[tile - kNumCfgsBf16];
   return d->kh == h.kh && d->kw == h.kw && d->stride_h == 1 && d->stride_w == 1 && d->ho == d->h &&
-         d->wo == d->w && d->c_in % chunk == 0 && halo_rows(d, h.t.bm) * (d->w + d->kw - 1) < h.slots;
+         d->wo == d->w && d->c_in % 32 == 0 && halo_rows(d, h.t.bm) * (d->w + d->kw - 1) < h.slots;
 }
 
 static void dgrad_phases(const jr_conv_desc* d, Phase* ph, int* nph) {
@@ -1316,13 +1307,10 @@ static int run_gemm(int dtype, ConvArgs a, const Plan& p, void* out, void* ws, s
     grid = dim3(p.sk_blocks, members, 1);
   }
   if (is_halo(dtype, p.tile)) {
-    const HaloCfg& h = halo_cfg(dtype, p.tile);
+    const HaloCfg& h = kHaloBf16[p.tile - kNumCfgsBf16];
     a.halo_wp = a.w + a.kw - 1;
     a.halo_nr = (h.t.bm + a.wo - 2) / a.wo + 1 + a.kh - 1;
-    if (dtype == JR_F32_X6H)
-      launch_conv_halo_h6(p.tile - 3 * kNumCfgs, a, grid, s);
-    else
-      launch_conv_halo(p.tile - kNumCfgsBf16, a, grid, s);
+    launch_conv_halo(p.tile - kNumCfgsBf16, a, grid, s);
   } else if (bf16_operands(dtype)) {
     // operand address mode (k_conv_bf16 AM): the tap is wave-uniform when the
     // reduction channel radix is a multiple of BK (0), else every piece walks

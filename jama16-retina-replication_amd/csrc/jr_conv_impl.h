@@ -808,22 +808,6 @@ static constexpr HaloCfg kHaloBf16[] = {
 };
 constexpr int kNumHaloBf16 = sizeof(kHaloBf16) / sizeof(kHaloBf16[0]);
 void launch_conv_halo(int h, const ConvArgs& a, dim3 grid, hipStream_t s);
-// JR_F32_X6H halo configs (jr_conv_halo_h6.hip): 16 fp32 channels per chunk
-// (64-byte slots); bk = taps x 16 (K-tiles = c_in / 16).  LDS per stage:
-// slots x 64 B + taps x 16 x BN x 4 B.
-static constexpr HaloCfg kHaloF32[] = {
-    {1, 7, 224, {128, 64, 2, 7 * 16, 2, 1.0}},    // 0: 17^2 1x7: 9 x 23 = 207 slots; 2 x 42 KiB
-    {7, 1, 256, {128, 64, 2, 7 * 16, 2, 1.0}},    // 1: 17^2 7x1: 15 x 17 = 255 slots; 2 x 44 KiB
-    {3, 3, 272, {128, 96, 4, 9 * 16, 2, 1.0}},    // 2: 35^2 3x3, N = 96: 7 x 37 = 259 slots; 2 x 71 KiB
-    {3, 3, 272, {128, 64, 2, 9 * 16, 2, 1.0}},    // 3: 3x3, N = 64 tiles (8^2: 18 x 10 = 180 slots); 2 x 53 KiB
-    {1, 3, 176, {128, 64, 2, 3 * 16, 3, 1.0}},    // 4: 8^2 1x3: 16 x 10 = 160 slots; 3 x 23 KiB
-    {3, 1, 160, {128, 64, 2, 3 * 16, 3, 1.0}},    // 5: 8^2 3x1: 18 x 8 = 144 slots; 3 x 22 KiB
-    {1, 7, 224, {128, 128, 2, 7 * 16, 2, 1.0}},   // 6: as 0, N = 128: 2 x 71 KiB
-    {7, 1, 256, {128, 128, 2, 7 * 16, 2, 1.0}},   // 7: as 1, N = 128: 2 x 73 KiB
-    {3, 3, 608, {128, 64, 2, 9 * 16, 2, 1.0}},    // 8: 147^2 3x3 (conv2d_3): 4 x 149 = 596 slots; 2 x 74 KiB
-};
-constexpr int kNumHaloF32 = sizeof(kHaloF32) / sizeof(kHaloF32[0]);
-void launch_conv_halo_h6(int h, const ConvArgs& a, dim3 grid, hipStream_t s);
 // conv2d_1 as a direct VALU convolution (jr_conv_direct.hip): the geometry
 // test, its statistics partials (P of R rows) and the launch (stats may be
 // nullptr; members > 1: blockIdx.y, byte strides)

@@ -114,7 +114,7 @@ def test_x6h_every_tile_config(case):
     wsb += 3 * 4 * max(n * ho * wo * cout, kh * kw * cin * cout, n * h * w * cin)
     ws = torch.zeros(wsb // 4 + 4, device="cuda")
     ncfg = L.jr_conv2d_num_configs(X6H)
-    assert ncfg > L.jr_conv2d_num_configs(2)          # + the halo-tiled forward ids (forward only, where they fit)
+    assert ncfg == L.jr_conv2d_num_configs(2)
     try:
         for cfg in [t | (sp << 8) for t in range(ncfg) for sp in (0, 3)]:
             for op in (0, 2):
@@ -229,51 +229,3 @@ def test_bn_backward_absmax_is_bitwise_and_exact(c):
     (dx0, db0, _), (dx1, db1, w1) = outs
     assert torch.equal(dx0, dx1) and torch.equal(db0, db1)
     assert float(w1.max()) == float(dx1.abs().max()) > 0
-
-
-# the halo-tiled forward ids (kHaloF32, ids 42..50) on the geometries they
-# are for: (case, halo index)
-HALO = [((2, 17, 17, 128, 192, 1, 7, 1, "same"), 0), ((2, 17, 17, 160, 192, 7, 1, 1, "same"), 1),
-        ((2, 35, 35, 64, 96, 3, 3, 1, "same"), 2), ((2, 8, 8, 448, 384, 3, 3, 1, "same"), 3),
-        ((2, 8, 8, 384, 384, 1, 3, 1, "same"), 4), ((2, 8, 8, 384, 384, 3, 1, 1, "same"), 5),
-        ((2, 17, 17, 192, 192, 1, 7, 1, "same"), 6), ((2, 17, 17, 128, 128, 7, 1, 1, "same"), 7),
-        ((2, 147, 147, 32, 64, 3, 3, 1, "same"), 8), ((1, 35, 35, 48, 64, 3, 3, 1, "same"), 3)]
-
-
-@pytest.mark.parametrize("case,h", HALO)
-def test_x6h_halo_forward_at_fp32_bars(case, h):
-    """Each halo config on its geometry (ragged tiles across images, the
-    row-edge zero slot, N tails), with the planner's split-K and forced
-    factors: y and the fused BN statistics against fp64 at the fp32 bars,
-    and bitwise the same halo call twice."""
-    ffi = _lib()
-    L = ffi.load()
-    n, hh, w, cin, cout, kh, kw, s, pad = case
-    d, (x, wt, dy), (X, W, DY), keep = _setup(ffi, case, 100 + h)
-    ref = R.conv2d(x, wt, s, pad)
-    base = L.jr_conv2d_num_configs(2)
-    wsb = L.jr_conv2d_workspace_size(ctypes.byref(d), 0, X6H) + 4 * 4 * ref.size + (1 << 20)
-    ws = torch.zeros(wsb // 4 + 4, device="cuda")
-    try:
-        for sp in (0, 1, 3):
-            cfg = (base + h) | (sp << 8)
-            ffi.check("set", L.jr_conv2d_set_config(ctypes.byref(d), 0, X6H, 0, cfg))
-            assert L.jr_conv2d_get_config(ctypes.byref(d), 0, X6H, 0) == cfg
-            outs = []
-            for _ in range(2):
-                Y = torch.zeros(ref.size, device="cuda")
-                st = torch.zeros(2 * cout, device="cuda")
-                ffi.check("fwd", L.jr_conv2d_fwd_bn_stats(ctypes.byref(d), X6H, X.data_ptr(), W.data_ptr(),
-                                                          Y.data_ptr(), 1e-3, st.data_ptr(), st.data_ptr() + 4 * cout,
-                                                          ws.data_ptr(), wsb, None))
-                torch.cuda.synchronize()
-                outs.append((Y.clone(), st.clone()))
-            assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-            got = outs[0][0].cpu().numpy().reshape(ref.shape)
-            assert relerr(got, ref) < 5e-6, (sp, relerr(got, ref))
-            r2 = ref.reshape(-1, cout).astype(np.float64)
-            mean = outs[0][1][:cout].cpu().numpy()
-            assert np.max(np.abs(mean - r2.mean(0))) <= 1e-5 * np.abs(r2).max(), sp
-        ffi.device_check()
-    finally:
-        ffi.check("reset", L.jr_conv2d_set_config(ctypes.byref(d), 0, X6H, 0, -1))
