@@ -26,7 +26,7 @@ from jr.engine import Engine  # noqa: E402
 # (dtype, conv_math, batch, res, train): BASELINE configs 2, 3, 4 (f32 / bf16 members), 5
 WORKLOADS = [("f32", "x8", 64, 299, True), ("bf16", "bf16", 64, 299, True), ("f32", "x8", 32, 299, False),
              ("bf16", "bf16", 32, 299, False), ("bf16", "bf16", 64, 587, True), ("f32", "x8p", 64, 299, True),
-             ("f32", "x6h", 64, 299, True)]
+             ("f32", "x6h", 64, 299, True), ("f32", "x6h", 32, 299, False)]
 REPS = 3
 
 
