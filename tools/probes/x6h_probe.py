@@ -4,6 +4,9 @@ the shipping JR_F32_X8 (bf16 split, eight MFMAs), same tile, one GEMM at a
 time: time per call (interleaved) and error vs an fp64 reference, with the
 fp32-MFMA kernel (JR_F32) as the fp32 yardstick.  Gate: error within x8's
 class and >= 15 % faster per GEMM.
+Historical: ran at eb5182a (profiles/r06_x6h_probe.txt); its debug entry point
+jr_debug_x8_f16 was removed once the split shipped as JR_F32_X6H (dtype 4,
+tests/test_gpu_x6h.py), so it no longer runs against the current libjr.
   python tools/probes/x6h_probe.py [reps]"""
 import ctypes
 import math
