@@ -120,7 +120,7 @@ struct SplitFrag {
   __device__ __forceinline__ bf16x8 l() const { return __builtin_bit_cast(bf16x8, (u32x4){lp[0], lp[1], lp[2], lp[3]}); }
 };
 
-// H6 probe (jr_debug_x8_f16): the same three-way split
+// JR_F32_X6H (H6): the same three-way split
 // into fp16 (11-bit significands) of the operand scaled by a power of two
 // (so its largest magnitude sits in [2^14, 2^15)): x s = h + m + l with h =
 // rtz(x s), m = rtz(x s - h), l = x s - h - m -- every remainder exact in
@@ -135,6 +135,22 @@ __device__ __forceinline__ uint32_t pkrtz_f16(float a, float b) {   // v_cvt_pkr
   return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
 }
 
+// x - (f32) f16 half of a packed pair in ONE v_fma_mix_f32 (-h * 1.0 + x, the
+// f16 source converted inside the instruction): exact, since h is x
+// truncated to fp16 precision and x - h is x's own low significand bits, so
+// bitwise the v_cvt_f32_f16 + v_sub_f32 pair it replaces at half the VALU
+// issue (the split's residual stages were 5 VALU per pair, now 3).
+__device__ __forceinline__ float sub_f16lo(float x, uint32_t h) {
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
+  return r;
+}
+__device__ __forceinline__ float sub_f16hi(float x, uint32_t h) {
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
+  return r;
+}
+
 struct SplitFrag16 {
   float x[8];
   uint32_t hp[4], mp[4], lp[4];
@@ -144,25 +160,19 @@ struct SplitFrag16 {
 #pragma unroll
     for (int p = 0; p < 4; ++p) hp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
   }
-  __device__ __forceinline__ static float lo(uint32_t u) {
-    return (float)__builtin_bit_cast(f16x2, u)[0];
-  }
-  __device__ __forceinline__ static float hi(uint32_t u) {
-    return (float)__builtin_bit_cast(f16x2, u)[1];
-  }
   __device__ __forceinline__ void stage2() {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      x[2 * p] = sub_f32(x[2 * p], lo(hp[p]));
-      x[2 * p + 1] = sub_f32(x[2 * p + 1], hi(hp[p]));
+      x[2 * p] = sub_f16lo(x[2 * p], hp[p]);
+      x[2 * p + 1] = sub_f16hi(x[2 * p + 1], hp[p]);
       mp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
     }
   }
   __device__ __forceinline__ void stage3() {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      x[2 * p] = sub_f32(x[2 * p], lo(mp[p]));
-      x[2 * p + 1] = sub_f32(x[2 * p + 1], hi(mp[p]));
+      x[2 * p] = sub_f16lo(x[2 * p], mp[p]);
+      x[2 * p + 1] = sub_f16hi(x[2 * p + 1], mp[p]);
       lp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
     }
   }

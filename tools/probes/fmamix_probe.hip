@@ -1,0 +1,97 @@
+// The JR_F32_X6H split's residual step, x - (f32) f16(h), as one
+// v_fma_mix_f32 (jr_conv.hip sub_f16lo / sub_f16hi) against the
+// v_cvt_f32_f16 + v_sub_f32 pair it replaced: bitwise over 2^24 scaled
+// operands per magnitude band (fp32 normals and subnormals, f16 normal and
+// subnormal ranges, both signs), all three split terms compared.
+//   hipcc --offload-arch=gfx950 -O3 tools/probes/fmamix_probe.hip -o /tmp/fmamix && /tmp/fmamix
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstring>
+
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pkrtz(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+}
+__device__ __forceinline__ float sub_ref(float x, float h) {
+  float r;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(h));
+  return r;
+}
+__device__ __forceinline__ float sub_lo(float x, uint32_t h) {
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
+  return r;
+}
+__device__ __forceinline__ float sub_hi(float x, uint32_t h) {
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
+  return r;
+}
+
+__device__ __forceinline__ uint32_t hash(uint32_t v) {
+  v ^= v >> 16; v *= 0x7feb352d; v ^= v >> 15; v *= 0x846ca68b; v ^= v >> 16;
+  return v;
+}
+
+// one pair (x0, x1) per thread; band b sets the exponent range of the scaled value
+__global__ void k_probe(uint32_t seed, int band, unsigned long long* bad, unsigned long long* first) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t r0 = hash(i * 2 + seed), r1 = hash(i * 2 + 1 + seed * 7919);
+  // exponent in [e0, e0 + 30): bands cover fp32 subnormals .. 2^15
+  const int e0 = band == 0 ? 1 : band == 1 ? 80 : band == 2 ? 100 : 112;
+  const uint32_t u0 = (r0 & 0x807fffffu) | ((uint32_t)(e0 + (r0 >> 8) % 30) << 23);
+  const uint32_t u1 = (r1 & 0x807fffffu) | ((uint32_t)(e0 + (r1 >> 8) % 30) << 23);
+  float a0 = __uint_as_float(band == 0 && (r0 & 1) ? (u0 & 0x807fffffu) : u0);   // some fp32 subnormals
+  float a1 = __uint_as_float(u1);
+  if (a0 != a0 || a1 != a1) return;
+  // reference split (the pre-fma_mix code)
+  uint32_t h = pkrtz(a0, a1);
+  float x0 = sub_ref(a0, (float)__builtin_bit_cast(f16x2, h)[0]);
+  float x1 = sub_ref(a1, (float)__builtin_bit_cast(f16x2, h)[1]);
+  uint32_t m = pkrtz(x0, x1);
+  float y0 = sub_ref(x0, (float)__builtin_bit_cast(f16x2, m)[0]);
+  float y1 = sub_ref(x1, (float)__builtin_bit_cast(f16x2, m)[1]);
+  uint32_t l = pkrtz(y0, y1);
+  // fma_mix split
+  uint32_t h2 = pkrtz(a0, a1);
+  float p0 = sub_lo(a0, h2), p1 = sub_hi(a1, h2);
+  uint32_t m2 = pkrtz(p0, p1);
+  float q0 = sub_lo(p0, m2), q1 = sub_hi(p1, m2);
+  uint32_t l2 = pkrtz(q0, q1);
+  const bool ok = h == h2 && m == m2 && l == l2 && __float_as_uint(x0) == __float_as_uint(p0) &&
+                  __float_as_uint(x1) == __float_as_uint(p1) && __float_as_uint(y0) == __float_as_uint(q0) &&
+                  __float_as_uint(y1) == __float_as_uint(q1);
+  if (!ok) {
+    const unsigned long long n = atomicAdd(bad, 1ull);
+    if (n == 0) *first = ((unsigned long long)__float_as_uint(a0) << 32) | __float_as_uint(a1);
+  }
+}
+
+int main() {
+  unsigned long long *bad, *first;
+  hipMalloc(&bad, 8);
+  hipMalloc(&first, 8);
+  int fails = 0;
+  for (int band = 0; band < 4; ++band) {
+    for (uint32_t seed = 1; seed <= 4; ++seed) {
+      hipMemset(bad, 0, 8);
+      hipMemset(first, 0, 8);
+      hipLaunchKernelGGL(k_probe, dim3(1 << 14), dim3(256), 0, 0, seed, band, bad, first);
+      unsigned long long hb = 0, hf = 0;
+      hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost);
+      hipMemcpy(&hf, first, 8, hipMemcpyDeviceToHost);
+      if (hipDeviceSynchronize() != hipSuccess) { printf("hip error\n"); return 2; }
+      uint32_t a = (uint32_t)(hf >> 32), b = (uint32_t)hf;
+      float fa, fb;
+      memcpy(&fa, &a, 4);
+      memcpy(&fb, &b, 4);
+      printf("band %d seed %u: %d pairs, %llu differ%s", band, seed, 1 << 22, hb, hb ? "" : "\n");
+      if (hb) printf(" (first: %g %g)\n", fa, fb);
+      fails += hb != 0;
+    }
+  }
+  printf(fails ? "FAIL\n" : "bitwise: all pairs equal\n");
+  return fails ? 1 : 0;
+}
