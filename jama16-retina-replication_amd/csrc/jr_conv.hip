@@ -135,20 +135,21 @@ __device__ __forceinline__ uint32_t pkrtz_f16(float a, float b) {   // v_cvt_pkr
   return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
 }
 
-// x - (f32) f16 half of a packed pair in ONE v_fma_mix_f32 (-h * 1.0 + x, the
+// x - (f32) f16 half of a packed pair in ONE v_fma_mix_f32 (-h * one + x, the
 // f16 source converted inside the instruction): exact, since h is x
 // truncated to fp16 precision and x - h is x's own low significand bits, so
 // bitwise the v_cvt_f32_f16 + v_sub_f32 pair it replaces at half the VALU
-// issue (the split's residual stages were 5 VALU per pair, now 3).
-__device__ __forceinline__ float sub_f16lo(float x, uint32_t h) {
-  float r;
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
-  return r;
+// issue (the residual stages were 5 VALU per pair, now 3).  `one` is 1.0
+// hidden from the optimiser (H6 prologue): with a literal 1.0 the fma folds to
+// fsub and hipcc emits the cvt + sub pair again; kept compiler-visible (not
+// inline asm) so the hazard pass sees a mix instruction -- its result needs
+// one wait state before a VALU reads it, so every stage issues all eight
+// residuals before its four packs.
+__device__ __forceinline__ float sub_f16lo(float x, uint32_t h, float one) {
+  return __builtin_fmaf(-(float)__builtin_bit_cast(f16x2, h)[0], one, x);
 }
-__device__ __forceinline__ float sub_f16hi(float x, uint32_t h) {
-  float r;
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
-  return r;
+__device__ __forceinline__ float sub_f16hi(float x, uint32_t h, float one) {
+  return __builtin_fmaf(-(float)__builtin_bit_cast(f16x2, h)[1], one, x);
 }
 
 struct SplitFrag16 {
@@ -160,21 +161,23 @@ struct SplitFrag16 {
 #pragma unroll
     for (int p = 0; p < 4; ++p) hp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
   }
-  __device__ __forceinline__ void stage2() {
+  __device__ __forceinline__ void stage2(float one) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      x[2 * p] = sub_f16lo(x[2 * p], hp[p]);
-      x[2 * p + 1] = sub_f16hi(x[2 * p + 1], hp[p]);
-      mp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
+      x[2 * p] = sub_f16lo(x[2 * p], hp[p], one);
+      x[2 * p + 1] = sub_f16hi(x[2 * p + 1], hp[p], one);
     }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) mp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
   }
-  __device__ __forceinline__ void stage3() {
+  __device__ __forceinline__ void stage3(float one) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      x[2 * p] = sub_f16lo(x[2 * p], mp[p]);
-      x[2 * p + 1] = sub_f16hi(x[2 * p + 1], mp[p]);
-      lp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
+      x[2 * p] = sub_f16lo(x[2 * p], mp[p], one);
+      x[2 * p + 1] = sub_f16hi(x[2 * p + 1], mp[p], one);
     }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) lp[p] = pkrtz_f16(x[2 * p], x[2 * p + 1]);
   }
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   __device__ __forceinline__ f16x8 h() const { return __builtin_bit_cast(f16x8, (u32x4){hp[0], hp[1], hp[2], hp[3]}); }
@@ -236,8 +239,9 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // JR_F32_X6H operand scales (wave-uniform)
-  float h_sa = 1.f, h_sb = 1.f;
+  float h_sa = 1.f, h_sb = 1.f, h_one = 1.f;
   if constexpr (H6) {
+    asm volatile("" : "+s"(h_one));      // SplitFrag16: 1.0 the optimiser cannot fold
     h_sa = __uint_as_float(__builtin_amdgcn_readfirstlane(
         __float_as_uint(pow2_scale(g.a_max ? absmax64(g.a_max, lane) : g.a_bnd))));
     h_sb = __uint_as_float(__builtin_amdgcn_readfirstlane(
@@ -635,7 +639,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) mmh(i, j, sa[i].h(), sb[j].h());
 #pragma unroll
-          for (int i = 0; i < TM; ++i) sa[i].stage2();
+          for (int i = 0; i < TM; ++i) sa[i].stage2(h_one);
           next_piece();
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -643,7 +647,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) mmh(i, j, sa[i].m(), sb[j].h());
 #pragma unroll
-          for (int j = 0; j < TN; ++j) sb[j].stage2();
+          for (int j = 0; j < TN; ++j) sb[j].stage2(h_one);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int i = 0; i < TM; ++i)
@@ -653,7 +657,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
               mmh(i, j, sa[i].m(), sb[j].m());
             }
 #pragma unroll
-          for (int i = 0; i < TM; ++i) sa[i].stage3();
+          for (int i = 0; i < TM; ++i) sa[i].stage3(h_one);
           next_piece();
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -661,7 +665,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) mmh(i, j, sa[i].l(), sb[j].h());
 #pragma unroll
-          for (int j = 0; j < TN; ++j) sb[j].stage3();
+          for (int j = 0; j < TN; ++j) sb[j].stage3(h_one);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int i = 0; i < TM; ++i)

@@ -1,5 +1,6 @@
 // The JR_F32_X6H split's residual step, x - (f32) f16(h), as one
-// v_fma_mix_f32 (jr_conv.hip sub_f16lo / sub_f16hi) against the
+// v_fma_mix_f32 (jr_conv.hip sub_f16lo / sub_f16hi: fma(-h, one, x), one = an
+// opaque 1.0) against the
 // v_cvt_f32_f16 + v_sub_f32 pair it replaced: bitwise over 2^24 scaled
 // operands per magnitude band (fp32 normals and subnormals, f16 normal and
 // subnormal ranges, both signs), all three split terms compared.
@@ -19,15 +20,11 @@ __device__ __forceinline__ float sub_ref(float x, float h) {
   asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(h));
   return r;
 }
-__device__ __forceinline__ float sub_lo(float x, uint32_t h) {
-  float r;
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
-  return r;
+__device__ __forceinline__ float sub_lo(float x, uint32_t h, float one) {   // as jr_conv.hip sub_f16lo
+  return __builtin_fmaf(-(float)__builtin_bit_cast(f16x2, h)[0], one, x);
 }
-__device__ __forceinline__ float sub_hi(float x, uint32_t h) {
-  float r;
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
-  return r;
+__device__ __forceinline__ float sub_hi(float x, uint32_t h, float one) {
+  return __builtin_fmaf(-(float)__builtin_bit_cast(f16x2, h)[1], one, x);
 }
 
 __device__ __forceinline__ uint32_t hash(uint32_t v) {
@@ -55,10 +52,12 @@ __global__ void k_probe(uint32_t seed, int band, unsigned long long* bad, unsign
   float y1 = sub_ref(x1, (float)__builtin_bit_cast(f16x2, m)[1]);
   uint32_t l = pkrtz(y0, y1);
   // fma_mix split
+  float one = 1.f;
+  asm volatile("" : "+s"(one));
   uint32_t h2 = pkrtz(a0, a1);
-  float p0 = sub_lo(a0, h2), p1 = sub_hi(a1, h2);
+  float p0 = sub_lo(a0, h2, one), p1 = sub_hi(a1, h2, one);
   uint32_t m2 = pkrtz(p0, p1);
-  float q0 = sub_lo(p0, m2), q1 = sub_hi(p1, m2);
+  float q0 = sub_lo(p0, m2, one), q1 = sub_hi(p1, m2, one);
   uint32_t l2 = pkrtz(q0, q1);
   const bool ok = h == h2 && m == m2 && l == l2 && __float_as_uint(x0) == __float_as_uint(p0) &&
                   __float_as_uint(x1) == __float_as_uint(p1) && __float_as_uint(y0) == __float_as_uint(q0) &&
