@@ -252,9 +252,14 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
 
   // SK: this block's iteration range [sk_it, sk_end) over tiles x K-tiles
   long long sk_it = 0, sk_end = 0;
+  // SK: logical block lb = xcd_remap(blockIdx.x): the blocks of one XCD walk
+  // adjacent iteration ranges, so a cut tile's pieces and the operand rows
+  // neighbouring ranges share stay in that XCD's L2 (the decomposition, and
+  // so every sum, is the same as with lb = blockIdx.x)
+  const int lb = SK ? xcd_remap(blockIdx.x, gridDim.x) : 0;
   if constexpr (SK) {
     const long long W = (long long)((g.M + BM - 1) / BM) * g.ntn * g.ktiles;
-    sk_it = (long long)blockIdx.x * g.sk_ipb;
+    sk_it = (long long)lb * g.sk_ipb;
     sk_end = sk_it + g.sk_ipb < W ? sk_it + g.sk_ipb : W;
   }
   bool sk_first = true;
@@ -815,7 +820,8 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   if constexpr (SK) {
     sk_first = false;
     int owner, npieces, kind;
-    if (sk_cut(g, tile, kt0, kt1, &owner, &npieces, &kind) && !sk_handoff<TM, TN>(g, acc, wave, lane, owner, npieces, kind))
+    if (sk_cut(g, tile, kt0, kt1, &owner, &npieces, &kind) &&
+        !sk_handoff<TM, TN>(g, acc, wave, lane, owner, npieces, kind, lb))
       continue;                      // another block finishes the tile
   }
   // ---------------------------------------------------------------- epilogue

@@ -80,9 +80,10 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
   const int wn0 = (wave % WGN) * WN;
 
   long long sk_it = 0, sk_end = 0;
+  const int lb = SK ? xcd_remap(blockIdx.x, gridDim.x) : 0;   // logical block (jr_conv.hip k_conv)
   if constexpr (SK) {
     const long long W = (long long)((g.M + BM - 1) / BM) * g.ntn * g.ktiles;
-    sk_it = (long long)blockIdx.x * g.sk_ipb;
+    sk_it = (long long)lb * g.sk_ipb;
     sk_end = sk_it + g.sk_ipb < W ? sk_it + g.sk_ipb : W;
   }
   bool sk_first = true;
@@ -517,7 +518,7 @@ __global__ void __launch_bounds__(NW * 64) k_conv_bf16(ConvArgs g) {
     sk_first = false;
     int owner, npieces, kind;
     if (sk_cut(g, tile, kt0, kt1, &owner, &npieces, &kind) &&
-        !sk_handoff<TM, TN, NW>(g, acc, wave, lane, owner, npieces, kind))
+        !sk_handoff<TM, TN, NW>(g, acc, wave, lane, owner, npieces, kind, lb))
       continue;                      // another block finishes the tile
   }
   // ---------------------------------------------------------------- epilogue

@@ -290,9 +290,10 @@ __device__ __forceinline__ void sk_sum_pieces(const ConvArgs& g, f32x16 (&acc)[T
 
 constexpr unsigned kSkOwnerBit = 1u << 16;   // low 16 bits: pieces published
 
+// lb: the block's logical index (its iteration range; xcd_remap of blockIdx.x)
 template <int TM, int TN, int NW = 4>
 __device__ __forceinline__ bool sk_handoff(const ConvArgs& g, f32x16 (&acc)[TM][TN], int wave, int lane, int owner,
-                                           int npieces, int kind) {
+                                           int npieces, int kind, int lb) {
   // s_state: 0 move on, 1 finish with the owner's piece in registers, 2 finish loading every piece
   __shared__ int s_state;
   unsigned* word = g.sk_flags + owner;
@@ -313,7 +314,7 @@ __device__ __forceinline__ bool sk_handoff(const ConvArgs& g, f32x16 (&acc)[TM][
     __syncthreads();
   }
   if (st == 0) {            // publish this piece, then count it
-    sk_store_piece<TM, TN, NW>(g, acc, wave, lane, 2LL * blockIdx.x + kind);
+    sk_store_piece<TM, TN, NW>(g, acc, wave, lane, 2LL * lb + kind);
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned old = __hip_atomic_fetch_add(word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
