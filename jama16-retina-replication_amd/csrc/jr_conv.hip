@@ -437,7 +437,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
         }
         const int hmax = OP == OP_FWD ? g.h : g.ho, wmax = OP == OP_FWD ? g.w : g.wo;
         const bool ok = (unsigned)(a_p0[i] + dr) < (unsigned)hmax && (unsigned)(a_p1[i] + dc) < (unsigned)wmax;
-        dma16(ok ? a_ptr[i] + off : zp, As + j * 256);
+        dma16_ring(ok ? a_ptr[i] + off : zp, As + j * 256);
       } else {
         const float* src = zp;
         if constexpr (OP == OP_FWD) {
@@ -473,7 +473,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
           src = ok ? p : zp;
           adv_mixed(a_s2[i], a_s1[i], a_s0[i], g.wo, g.ho, a_multi);
         }
-        dma16(src, As + j * 256);
+        dma16_ring(src, As + j * 256);
       }
       return;
     }
@@ -483,12 +483,12 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     if constexpr (B_KC) {  // DGRAD: W[(r0+sh*a, c0+sw*bb)][ci][co]
       if constexpr (ut) {
         const long long off = (long long)((g.r0 + g.sh * t_r) * g.kw + (g.c0 + g.sw * t_c)) * g.cin * g.cout + t_ch;
-        dma16(b_p0[i] >= 0 ? b_ptr[i] + off : zp, Bs + j * 256);
+        dma16_ring(b_p0[i] >= 0 ? b_ptr[i] + off : zp, Bs + j * 256);
       } else {
         const bool ok = b_p0[i] >= 0 && b_s0[i] < g.na;
         const int r = g.r0 + g.sh * b_s0[i], c = g.c0 + g.sw * b_s1[i];
         const float* p = g.B + (((r * g.kw + c) * g.cin + b_p0[i]) * g.cout + b_s2[i]);
-        dma16(ok ? p : zp, Bs + j * 256);
+        dma16_ring(ok ? p : zp, Bs + j * 256);
         adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
       }
     } else {
@@ -504,7 +504,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
           p = g.B + ((rc * g.cin + ci) * g.N + b_p0[i]);
         }
       }
-      dma16(ok ? p : zp, Bs + j * 256);
+      dma16_ring(ok ? p : zp, Bs + j * 256);
     }
   };
   // advance the wave-uniform tap by BK after a tile's pieces are issued

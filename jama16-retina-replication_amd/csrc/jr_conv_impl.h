@@ -195,6 +195,25 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_chunk) {
                                    (__attribute__((address_space(3))) void*)lds_chunk, 16, 0, 0);
 }
 
+// The same LDS-DMA piece issued from inline asm, for k_conv, whose K loop
+// orders every DMA against the LDS reads itself (counted wait_vmcnt +
+// s_barrier per K-tile).  hipcc's waitcnt pass cannot see through the
+// stream-K hand-off: with the builtin it put an s_waitcnt vmcnt(0) before
+// the first LDS read of every K-tile in most stream-K kernels (168 of 518
+// k_conv steady loops; the non-stream-K twins had none), draining the ring's
+// prefetch each iteration; invisible to that pass, the DMA is waited for
+// where the kernel waits (117 loops lose the drain, none gain one; fp32 step
+// -0.5 %, profiles/r06_ab_dmaring.txt).  k_conv_bf16 keeps the builtin: its
+// step was 0.5 % slower this way.  m0 is written here only (the compiler
+// uses it for nothing else in these kernels: checked in the build's
+// assembly), and an SALU write of m0 needs one wait state before an LDS DMA
+// reads it (gfx9), hence the s_nop.
+__device__ __forceinline__ void dma16_ring(const void* src, void* lds_chunk) {
+  const uint32_t l = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) void*)lds_chunk);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(src), "s"(__builtin_amdgcn_readfirstlane(l)) : "memory");
+}
+
 // ---------------------------------------------------------------- stream-K
 // Hand-off of a cut tile's pieces (jr_conv.hip k_conv SK documents the
 // scheme; k_conv_bf16 uses the same).  No block ever waits for another:
