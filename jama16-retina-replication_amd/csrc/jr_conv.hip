@@ -767,6 +767,12 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
     }
   };
 
+  // every compiler-visible load of the previous segment (hand-off pieces,
+  // accumulate reads, the H6 magnitude words) retired here, once per
+  // segment: otherwise hipcc's waitcnt pass, which merges that state into
+  // the K loop, keeps an s_waitcnt vmcnt(0) in every K-tile (and so drains
+  // the DMA ring it cannot see)
+  __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0)
   if (kt0 < kt1) {
     // prologue: tiles kt0 .. kt0+NBUF-2 in flight
 #pragma unroll

@@ -202,8 +202,9 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_chunk) {
 // the first LDS read of every K-tile in most stream-K kernels (168 of 518
 // k_conv steady loops; the non-stream-K twins had none), draining the ring's
 // prefetch each iteration; invisible to that pass, the DMA is waited for
-// where the kernel waits (117 loops lose the drain, none gain one; fp32 step
-// -0.5 %, profiles/r06_ab_dmaring.txt).  k_conv_bf16 keeps the builtin: its
+// where the kernel waits, and with one explicit vmcnt(0) per stream-K
+// segment (k_conv) no steady loop keeps a drain (490 of 490; fp32 step
+// -0.8 %, profiles/r06_ab_dmaring.txt).  k_conv_bf16 keeps the builtin: its
 // step was 0.5 % slower this way.  m0 is written here only (the compiler
 // uses it for nothing else in these kernels: checked in the build's
 // assembly), and an SALU write of m0 needs one wait state before an LDS DMA
