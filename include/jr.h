@@ -100,13 +100,6 @@ typedef struct jr_conv_desc {
   const float* w_absmax;
   const float* dy_absmax;
   float x_bound, w_bound, dy_bound;
-  /* JR_F32_X6H forward only (NULL: split in the GEMM): the filter block's
-   * three fp16 split planes as jr_x6h_filter_planes writes them -- [3][K/2][N]
-   * uint32 pairs (k even, k odd) of rtz-split terms of w scaled by the
-   * power of two of w_absmax, K = kh*kw*c_in, N = c_out.  The GEMM then reads
-   * the planes instead of splitting the filters per K-tile; bitwise the same
-   * products.  Used where c_in is a multiple of 16 (else ignored). */
-  const void* w_planes;
 } jr_conv_desc;
 
 /* 3x3 pooling window; max: stride 2 'valid', avg: stride 1 'same' with the
@@ -466,19 +459,6 @@ typedef struct jr_absmax_seg {
 } jr_absmax_seg;
 int jr_absmax_prep(const float* src, const jr_absmax_seg* segs, int32_t nseg, float* out, int64_t zero_floats,
                    void* stream);
-
-/* JR_F32_X6H forward filters pre-split once per step (replaces
- * SplitFrag16's filter half inside the conv K loop; jr_conv_desc.w_planes):
- * segment i reads the fp32 filter block params[src_off .. + K*N) ([K][N],
- * K even), its power-of-two scale from the 64 words absmax[64*row ..], and
- * writes planes[dst_off ..] as [3][K/2][N] uint32 = (fp16 term of k even,
- * of k odd) for h, m, l: the split of jr_conv.hip SplitFrag16, bit for bit. */
-typedef struct jr_planes_seg {
-  int64_t src_off, dst_off;
-  int32_t k, n, row, pad;
-} jr_planes_seg;
-int jr_x6h_filter_planes(const jr_planes_seg* segs, int32_t nseg, const float* params, const float* absmax,
-                         void* planes, void* stream);
 
 /* ---- dtype helpers --------------------------------------------------- */
 int jr_cast_f32_to_bf16(const float* src, void* dst, int64_t n, void* stream);

@@ -214,7 +214,7 @@ struct SplitFrag16 {
 // count words are per-stream library words (stream_scratch) that the
 // completing block resets, so a launch needs no memset.
 template <int OP, int BM, int BN, int WGM, int BK, int NBUF, bool UT, bool X8, int DBG = 0, bool SK = false,
-          bool H6 = false, bool BP = false>
+          bool H6 = false>
 __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int WGN = 4 / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -226,11 +226,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
   constexpr int HALF = BK / 2;                // k per lane half
   constexpr bool A_KC = (OP != OP_WGRAD);
   constexpr bool B_KC = (OP == OP_DGRAD);
-  // BPL (JR_F32_X6H FWD with jr_conv_desc.w_planes): the B image is the
-  // filters' three pre-split fp16 planes, [3][BK/2][BN] uint32 pairs
-  constexpr bool BPL = BP && H6 && UT && OP == OP_FWD;
-  constexpr int PLW = (BK / 2) * BN;          // 4-byte words per plane image
-  constexpr int ASZ = BM * BK, BSZ = BPL ? 3 * PLW : BN * BK;  // 4-byte words per image
+  constexpr int ASZ = BM * BK, BSZ = BN * BK;  // floats per image
   constexpr int A_INSTR = ASZ / 256, B_INSTR = BSZ / 256;
   constexpr int A_PW = (A_INSTR + 3) / 4, B_PW = (B_INSTR + 3) / 4;  // per wave
   static_assert(ASZ % 256 == 0 && BSZ % 256 == 0, "tile must be whole DMA instructions");
@@ -398,14 +394,6 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
       b_s2[i] = k - ab * g.cout;
       b_s0[i] = ab / g.nb;
       b_s1[i] = ab - b_s0[i] * g.nb;
-    } else if constexpr (BPL) {  // planes: plane pl, rows = k pairs, cols = n
-      constexpr int PLI = PLW / 256;      // DMA instructions per plane image
-      const int pl = j / PLI, jj = j - pl * PLI;
-      const int flat = jj * 256 + lane * 4;
-      const int krow = flat / BN, col = flat - krow * BN;
-      b_p0[i] = (n0 + col < g.N) ? n0 + col : -1;
-      b_s0[i] = kt0 * (BK / 2) + krow;    // k pair of this lane at tile kt0
-      b_ptr[i] = reinterpret_cast<const float*>(g.bpl + pl * g.bpl_ps + (long long)b_s0[i] * g.N + (n0 + col));
     } else {  // MC: rows = k, cols = n
       const int flat = j * 256 + lane * 4;
       const int krow = flat / BN, col = flat - krow * BN;
@@ -503,10 +491,6 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
         dma16_ring(ok ? p : zp, Bs + j * 256);
         adv_mixed(b_s2[i], b_s1[i], b_s0[i], g.cout, g.nb, b_multi);
       }
-    } else if constexpr (BPL) {
-      const int dk = (kt - kt0) * (BK / 2);                        // wave-uniform
-      const bool ok = (b_p0[i] >= 0) & (b_s0[i] + dk < (g.K >> 1));
-      dma16_ring(ok ? b_ptr[i] + (long long)dk * g.N : zp, Bs + j * 256);
     } else {
       const int kbase = kt * BK;                                   // wave-uniform
       const long long off = (long long)(kbase - kt0 * BK) * (OP == OP_FWD ? g.N : g.ys);
@@ -595,7 +579,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
         }
       }
 #pragma unroll
-      for (int j = 0; j < (BPL ? 0 : TN); ++j) {
+      for (int j = 0; j < TN; ++j) {
         if constexpr (B_KC) {
           const int row = wn0 + j * 32 + l31;
           const int f = (row / SWZ) % QPR;
@@ -653,21 +637,8 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
           SplitFrag16 sa[TM], sb[TN];
 #pragma unroll
           for (int i = 0; i < TM; ++i) sa[i].init(&af[i][8 * g8], h_sa);
-          if constexpr (BPL) {      // the filters' terms as jr_x6h_filter_planes split them
-            const uint32_t* Bu = reinterpret_cast<const uint32_t*>(Bs);
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-              for (int t = 0; t < 4; ++t) {
-                const int o = ((lh * HALF + 8 * g8) / 2 + t) * BN + wn0 + j * 32 + l31;
-                sb[j].hp[t] = Bu[o];
-                sb[j].mp[t] = Bu[PLW + o];
-                sb[j].lp[t] = Bu[2 * PLW + o];
-              }
-          } else {
-#pragma unroll
-            for (int j = 0; j < TN; ++j) sb[j].init(&bfr[j][8 * g8], h_sb);
-          }
+          for (int j = 0; j < TN; ++j) sb[j].init(&bfr[j][8 * g8], h_sb);
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -681,7 +652,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) mmh(i, j, sa[i].m(), sb[j].h());
 #pragma unroll
-          for (int j = 0; j < (BPL ? 0 : TN); ++j) sb[j].stage2(h_one);
+          for (int j = 0; j < TN; ++j) sb[j].stage2(h_one);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int i = 0; i < TM; ++i)
@@ -699,7 +670,7 @@ __global__ void __launch_bounds__(256) k_conv(ConvArgs g) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) mmh(i, j, sa[i].l(), sb[j].h());
 #pragma unroll
-          for (int j = 0; j < (BPL ? 0 : TN); ++j) sb[j].stage3(h_one);
+          for (int j = 0; j < TN; ++j) sb[j].stage3(h_one);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int i = 0; i < TM; ++i)
@@ -1154,17 +1125,6 @@ template <int OP, int C, int DBG, bool X8, bool SK, bool H6 = false>
 static void launch_cfg(const ConvArgs& a, dim3 grid, hipStream_t s) {
   constexpr TileCfg t = kCfgs[C];
   const bool fast = OP == OP_WGRAD ? t.bk / a.wo < a.ho : (OP == OP_FWD ? a.cp : a.cout) % t.bk == 0;
-  // x6h FWD with pre-split filter planes, where the larger B image keeps two
-  // blocks per CU (not tiles 1 and 13)
-  constexpr bool bp_ok = OP == OP_FWD && H6 && DBG == 0 &&
-                         t.nbuf * (t.bm * t.bk + 3 * (t.bk / 2) * t.bn) * 4 <= 79 * 1024;
-  if constexpr (bp_ok) {
-    if (fast && a.bpl != nullptr) {
-      hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, X8, 0, SK, true, true>), grid, dim3(256), 0, s,
-                         a);
-      return;
-    }
-  }
   if (fast) {
     hipLaunchKernelGGL((k_conv<OP, t.bm, t.bn, t.wgm, t.bk, t.nbuf, true, X8, DBG, SK, H6>), grid, dim3(256), 0, s, a);
     return;
@@ -1244,11 +1204,7 @@ static void fill_scales(ConvArgs& a, const jr_conv_desc* d, int op, int dtype) {
   const float* xm = d->x_absmax;  const float xb = d->x_bound;
   const float* wm = d->w_absmax;  const float wb = d->w_bound;
   const float* gm = d->dy_absmax; const float gb = d->dy_bound;
-  if (op == OP_FWD) {
-    a.a_max = xm; a.a_bnd = xb; a.b_max = wm; a.b_bnd = wb;
-    a.bpl = static_cast<const uint32_t*>(d->w_planes);
-    a.bpl_ps = (long long)(d->kh * d->kw * d->c_in / 2) * d->c_out;
-  }
+  if (op == OP_FWD) { a.a_max = xm; a.a_bnd = xb; a.b_max = wm; a.b_bnd = wb; }
   else if (op == OP_DGRAD) { a.a_max = gm; a.a_bnd = gb; a.b_max = wm; a.b_bnd = wb; }
   else { a.a_max = xm; a.a_bnd = xb; a.b_max = gm; a.b_bnd = gb; }
 }
@@ -1822,49 +1778,6 @@ JR_API int jr_conv2d_bwd_filter_slabs(const jr_conv_desc* d, int dtype, const vo
   }
   a.c_off = 0; a.c_stride = d->c_out;
   return run_gemm<OP_WGRAD>(dtype, a, p, nullptr, slabs, slab_bytes, as_stream(stream), nullptr, true);
-}
-
-// JR_F32_X6H forward filters split once per step into the three fp16
-// planes k_conv's BPL path reads (jr.h jr_x6h_filter_planes): segment
-// blockIdx.y, pairs (k even, k odd) of one filter column per thread, the
-// scale and the split of SplitFrag16 (x = w s; h = rtz(x); m = rtz(x - h);
-// l = rtz(x - h - m); every remainder exact), contraction off so that x = w s
-// is rounded exactly as the GEMM's own v_mul_f32 rounds it.
-__global__ void __launch_bounds__(256) k_x6h_filter_planes(const jr_planes_seg* __restrict__ segs,
-                                                           const float* __restrict__ params,
-                                                           const float* __restrict__ absmax,
-                                                           uint32_t* __restrict__ planes) {
-#pragma clang fp contract(off)
-  const jr_planes_seg sg = segs[blockIdx.y];
-  const long long pairs = (long long)(sg.k / 2) * sg.n;
-  float mx = 0.f;
-  for (int t = 0; t < 64; ++t) mx = fmaxf(mx, absmax[64LL * sg.row + t]);
-  const float sc = pow2_scale(mx);
-  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < pairs; q += (long long)gridDim.x * 256) {
-    const long long kp = q / sg.n, nn = q - kp * sg.n;
-    const float* w = params + sg.src_off + 2 * kp * sg.n + nn;
-    float x0 = w[0] * sc, x1 = w[sg.n] * sc;
-    const uint32_t h = pkrtz_f16(x0, x1);
-    x0 = x0 - (float)__builtin_bit_cast(f16x2, h)[0];
-    x1 = x1 - (float)__builtin_bit_cast(f16x2, h)[1];
-    const uint32_t m = pkrtz_f16(x0, x1);
-    x0 = x0 - (float)__builtin_bit_cast(f16x2, m)[0];
-    x1 = x1 - (float)__builtin_bit_cast(f16x2, m)[1];
-    const uint32_t l = pkrtz_f16(x0, x1);
-    uint32_t* o = planes + sg.dst_off + q;
-    o[0] = h;
-    o[pairs] = m;
-    o[2 * pairs] = l;
-  }
-}
-
-JR_API int jr_x6h_filter_planes(const jr_planes_seg* segs, int32_t nseg, const float* params, const float* absmax,
-                                void* planes, void* stream) {
-  if (!segs || nseg <= 0 || nseg > 65535 || !params || !absmax || !planes)
-    return fail(JR_ERR_INVALID, "x6h_filter_planes: null argument or bad segment count");
-  hipLaunchKernelGGL(k_x6h_filter_planes, dim3(512, nseg), dim3(256), 0, as_stream(stream), segs, params, absmax,
-                     static_cast<uint32_t*>(planes));
-  return check_launch("x6h_filter_planes");
 }
 
 JR_API int jr_wgrad_reduce(const jr_wgrad_seg* segs, int32_t nseg, int32_t total_blocks, void* stream) {

@@ -62,10 +62,6 @@ struct ConvArgs {
   const float* a_max;
   const float* b_max;
   float a_bnd, b_bnd;
-  // JR_F32_X6H FWD: the filters' pre-split fp16 planes ([3][K/2][N] uint32
-  // pairs; jr_x6h_filter_planes), plane stride in uint32
-  const uint32_t* bpl;
-  long long bpl_ps;
 };
 
 // max of the 64 floats at p (every lane of the wave gets it)

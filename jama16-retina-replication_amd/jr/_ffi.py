@@ -40,8 +40,7 @@ class ConvDesc(Structure):
         "ho", "wo", "x_c_off", "x_c_stride", "y_c_off", "y_c_stride")] + [
         # JR_F32_X6H operand magnitude bounds (jr.h): absmax words or host bounds
         ("x_absmax", c_void_p), ("w_absmax", c_void_p), ("dy_absmax", c_void_p),
-        ("x_bound", ctypes.c_float), ("w_bound", ctypes.c_float), ("dy_bound", ctypes.c_float),
-        ("w_planes", c_void_p)]
+        ("x_bound", ctypes.c_float), ("w_bound", ctypes.c_float), ("dy_bound", ctypes.c_float)]
 
 
 class WPrep(Structure):
@@ -54,12 +53,6 @@ class WPrep(Structure):
 class AbsmaxSeg(Structure):
     """include/jr.h jr_absmax_seg: one parameter block of jr_absmax_prep."""
     _fields_ = [("off", c_int64), ("count", c_int64), ("out", c_int32), ("limit", c_float)]
-
-
-class PlanesSeg(Structure):
-    """include/jr.h jr_planes_seg: one filter block of jr_x6h_filter_planes."""
-    _fields_ = [("src_off", c_int64), ("dst_off", c_int64), ("k", c_int32), ("n", c_int32), ("row", c_int32),
-                ("pad", c_int32)]
 
 
 class BnSeg(Structure):
@@ -169,7 +162,6 @@ _SIGS = {
     "jr_bn_relu_bwd_multi_absmax": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int32,
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
     "jr_absmax_prep": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
-    "jr_x6h_filter_planes": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "jr_maxpool3x3s2_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p,
                                     c_void_p]),
     "jr_bn_relu_maxpool3x3s2_fwd": (c_int, [POINTER(PoolDesc), c_int, c_void_p, c_void_p, c_void_p, c_void_p,

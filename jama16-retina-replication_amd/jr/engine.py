@@ -327,8 +327,6 @@ class Engine:
         self.ws = self.ws_lane[0]
         if self.x6h:
             self._alloc_absmax(B)
-            if os.environ.get("JR_X6H_PLANES", "1") != "0":
-                self._alloc_filter_planes()
 
     def _alloc_absmax(self, B: int) -> None:
         """JR_F32_X6H magnitude words: 64 floats per conv launch for its
@@ -355,25 +353,6 @@ class Engine:
         arr = (_ffi.AbsmaxSeg * len(segs))(*segs)
         self.absmax_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
         self.absmax_nseg = len(segs)
-
-    def _alloc_filter_planes(self) -> None:
-        """JR_F32_X6H forward filters pre-split (jr_x6h_filter_planes, once
-        per step after jr_absmax_prep): three fp16 planes [3][K/2][N] per conv
-        launch whose c_in is a multiple of 16 (the GEMM's uniform-tap path),
-        so the forward GEMMs read the filters' terms instead of splitting
-        them in every K-tile (bitwise the same products)."""
-        segs, off, self._ploff = [], 0, {}
-        for k, u in enumerate(self.cunits):
-            if u.x == self.g.input_buf or u.cin % 16:
-                continue
-            K = u.kh * u.kw * u.cin
-            segs.append(_ffi.PlanesSeg(u.koff, off, K, u.cout, k, 0))
-            self._ploff[u.first.idx] = off
-            off += 3 * (K // 2) * u.cout
-        self.wplanes = torch.empty(max(off, 1), dtype=torch.int32, device=self.device)
-        arr = (_ffi.PlanesSeg * len(segs))(*segs)
-        self.planes_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
-        self.planes_nseg = len(segs)
 
     def _wmax(self, u: ConvUnit) -> int:
         return self.absmax.data_ptr() + 4 * 64 * self._arow[u.first.idx]
@@ -653,8 +632,6 @@ class Engine:
             d.x_bound = 1.0 if u.x == self.g.input_buf else self.act_bound    # images: f32(k) * f32(1/255) <= 1
             d.w_absmax = self._wmax(u)
             d.dy_absmax = self._dmax(u)
-            if getattr(self, "wplanes", None) is not None and u.first.idx in self._ploff:
-                d.w_planes = self.wplanes.data_ptr() + 4 * self._ploff[u.first.idx]
         return d
 
     def _pool_desc(self, n: PoolNode, B: int) -> _ffi.PoolDesc:
@@ -713,18 +690,12 @@ class Engine:
             add(fwd, *self._wprep_call(S[0]), 0, [("p",)], [("w16",)])
         # x6h: the convs read their filters' magnitude words besides the filters
         xw = [("wmax",)] if self.x6h else []
-        xpl = [("wpl",)] if getattr(self, "wplanes", None) is not None else []   # the forward's filter planes
         if self.x6h:
             # the filters' magnitudes (and the beta guard), and every
             # gradient row zeroed, before the first conv of the step
             add(fwd, L.jr_absmax_prep, (self.params.data_ptr(), self.absmax_table.data_ptr(), self.absmax_nseg,
                                         self.absmax.data_ptr(), self.absmax.numel(), S[0]), "absmax_prep", 0,
                 [("p",)], [("wmax",)] + [("dmax", u.first.idx) for u in self.cunits], nbytes=4 * self.nparam)
-            if getattr(self, "wplanes", None) is not None:
-                add(fwd, L.jr_x6h_filter_planes, (self.planes_table.data_ptr(), self.planes_nseg,
-                                                  self.params.data_ptr(), self.absmax.data_ptr(),
-                                                  self.wplanes.data_ptr(), S[0]), "x6h_filter_planes", 0,
-                    [("p",), ("wmax",)], [("wpl",)], nbytes=10 * self.nparam)
         # x8p: conv operands are the split planes of the input buffer, written
         # once (by the lane of its first consumer) when the buffer is complete
         AX = (lambda bid: self.aplanes[bid].data_ptr()) if x8p else A  # noqa: E731
@@ -764,7 +735,7 @@ class Engine:
                     # combines its channels' partials (and stores mean / invstd)
                     add(fwd, L.jr_conv2d_fwd_bn_partials, (ctypes.byref(d), cdt, AX(u.x), self._wf(u), raw, ws, wsb,
                                                            s),
-                        "conv_fwd", ln, ax_reads(u.x) + [wkey] + xw + xpl, [("r", uid), ("ws", ln)])
+                        "conv_fwd", ln, ax_reads(u.x) + [wkey] + xw, [("r", uid), ("ws", ln)])
                     part = ws.value + lay.ws_offset
                     for m, co in zip(u.members, u.col_off):
                         yb = g.bufs[m.y.buf]
@@ -779,7 +750,7 @@ class Engine:
                 add(fwd, L.jr_conv2d_fwd_bn_stats, (ctypes.byref(d), cdt, AX(u.x), self._wf(u), raw, BN_EPS,
                                                     self.mean_unit[uid].data_ptr(),
                                                     self.invstd_unit[uid].data_ptr(), ws, wsb, s),
-                    "conv_fwd", ln, ax_reads(u.x) + [wkey] + xw + xpl, [("r", uid), ("ws", ln)])
+                    "conv_fwd", ln, ax_reads(u.x) + [wkey] + xw, [("r", uid), ("ws", ln)])
                 if (self.apply_multi and len(u.members) > 1 and u.cout // self._vw <= 256
                         and not any(m.y.buf in fused_bufs for m in u.members)):
                     # every member's BN + ReLU in one launch (jr_bn_relu_apply_multi)

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: ran at e0ab593; the planes path and JR_X6H_PLANES were removed after this A/B)
 # x6h forward filters from pre-split planes: the bitwise test (planes vs the
 # in-loop split), then an interleaved same-box A/B of JR_X6H_PLANES=0 / 1.
 set -o pipefail
